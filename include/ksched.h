@@ -1,0 +1,157 @@
+/*
+ * ksched.h -- C ABI of the MI355X-native scheduling core (libksched.so).
+ *
+ * Drop-in boundary for the hot path of yinwoods/k8s-scheduler (paths relative to the reference):
+ *   func predicate(pod *Pod) ([]*Node, error)              anchor/predicate.go:107-176
+ *   func priorities(pod *Pod, nodes []*Node) (*Node, error) anchor/priorities.go:25-63
+ *   the per-pod commit that the next pod observes           anchor/schedule.go:68-89, 185-197
+ *                                                           (used += request, anchor/predicate.go:83-105)
+ * The Go caller keeps getNodes/getPods (anchor/tools.go:53-108) and bind/postEvent
+ * (anchor/schedule.go:200-261) unchanged; see INTEGRATION.md for the cgo shim.
+ *
+ * Plain C types only.  Caller-owned arrays are read (or written) during the call only and never
+ * retained, so Go slices of scalars may be passed directly under the cgo pointer rules.
+ * Every function returns an int status (KSCHED_OK == 0), never throws across the ABI and never
+ * exits the process.  A context is not reentrant: callers serialise calls on one context exactly as
+ * the reference serialises schedulePod under processorLock (anchor/schedule.go:29,55,186).
+ */
+#ifndef KSCHED_H
+#define KSCHED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSCHED_ABI_VERSION 1
+
+/* status codes */
+#define KSCHED_OK 0
+#define KSCHED_E_INVALID (-1)   /* bad argument / shape / option */
+#define KSCHED_E_DEVICE (-2)    /* HIP or RCCL failure, or a device-side timeout */
+#define KSCHED_E_PARSE (-3)     /* the reference's errFatal parse paths (anchor/predicate.go:15,31,39,49) */
+#define KSCHED_E_STATE (-4)     /* call out of order (e.g. schedule before load_nodes) */
+#define KSCHED_E_NOMEM (-5)
+#define KSCHED_E_UNKNOWN_NODE (-6) /* a bound pod names a node not in the node list (reference: nil deref panic, anchor/predicate.go:94-99) */
+
+/* per-pod outcome in out_idx[] */
+#define KSCHED_NO_FIT (-1)            /* predicate found no node: reference returns "failed to fit" (anchor/schedule.go:74-76) */
+#define KSCHED_NO_POSITIVE_SCORE (-2) /* no node scored > 0: reference binds a nil node and panics (anchor/priorities.go:55-62, anchor/schedule.go:208); documented divergence */
+
+/* options */
+#define KSCHED_MODE_EXACT 0     /* pod-by-pod: one full node scan + grid-wide arg-best per pod (persistent kernel) */
+#define KSCHED_MODE_BATCHED 1   /* speculative top-K for a batch of pods + ordered commit with exact re-score */
+#define KSCHED_MODE_AUTO 2
+
+#define KSCHED_PRIORITY_RESOURCE 0    /* (balanced + least-requested) / 2, anchor/priorities.go:45-50 */
+#define KSCHED_PRIORITY_BEST_PRICE 1  /* lowest node price among feasible nodes (README.md:37-64; build-defined) */
+
+#define KSCHED_DOMAIN_ALL 0       /* argmax over ALL nodes, feasible or not (the reference, anchor/priorities.go:45) */
+#define KSCHED_DOMAIN_FEASIBLE 1  /* argmax over feasible nodes only (build extension) */
+
+typedef struct ksched_opts {
+    int32_t struct_size; /* = sizeof(ksched_opts) */
+    int32_t mode;        /* KSCHED_MODE_* */
+    int32_t priority;    /* KSCHED_PRIORITY_* */
+    int32_t domain;      /* KSCHED_DOMAIN_* (best-price always ranges over feasible nodes) */
+    int32_t use_labels;  /* 1: feasible &= (node_labels & pod_selector) == pod_selector (build extension) */
+    int32_t batch;       /* batched mode: pods per speculative batch (0 = auto) */
+    int32_t topk;        /* batched mode: candidates kept per pod, one of 4, 8, 16 (0 = auto) */
+    int32_t device;      /* HIP device ordinal (-1 = current) */
+    /* node sharding across ranks (multi-GPU); single GPU: rank 0, nranks 1 */
+    int32_t rank;
+    int32_t nranks;
+    int64_t node_offset;  /* global index of this rank's first node */
+    int64_t nodes_global; /* total nodes across ranks (0 = local count when nranks == 1) */
+    int32_t exact_wgs;    /* exact mode: workgroups (0 = auto) */
+    int32_t reserved[7];
+} ksched_opts;
+
+typedef struct ksched_ctx ksched_ctx;
+
+typedef struct ksched_stats {
+    int64_t pods;          /* pods resolved by the last schedule call */
+    int64_t placed;        /* pods bound to a node */
+    int64_t batches;       /* speculative batches launched (batched mode) */
+    int64_t truncations;   /* batches cut short by a candidate-list overflow */
+    int64_t pair_evals;    /* pod-node pairs evaluated by the score kernels */
+    double device_ms;      /* device time of the last schedule call (HIP events) */
+    double kernel_ms[4];   /* per kernel family: [0] score/exact, [1] merge, [2] commit, [3] collective */
+    int64_t kernel_launches[4];
+} ksched_stats;
+
+/* ---- lifecycle ---- */
+int ksched_abi_version(void);
+int ksched_default_opts(ksched_opts *opts);
+int ksched_create(const ksched_opts *opts, ksched_ctx **out);
+int ksched_destroy(ksched_ctx *ctx);
+const char *ksched_last_error(const ksched_ctx *ctx); /* never NULL; "" when no error */
+
+/* Multi-GPU: rank 0 creates a 128-byte RCCL unique id; every rank passes it to ksched_set_comm
+ * before the first schedule call (opts.nranks > 1). */
+int ksched_get_unique_id(uint8_t out_id[128]);
+int ksched_set_comm(ksched_ctx *ctx, const uint8_t id[128]);
+
+/* ---- node state (allocatable = capacity - used, anchor/predicate.go:56-67) ---- */
+/* Loads this rank's n nodes (node order = nodeList.Items order).  labels / price may be NULL
+ * unless the options need them.  Prices must be finite. */
+int ksched_load_nodes(ksched_ctx *ctx, int64_t n, const int64_t *alloc_cpu, const int64_t *alloc_mem,
+                      const int64_t *alloc_pods, const uint64_t *labels, const float *price);
+/* alloc[node_idx[i]] += (d_cpu[i], d_mem[i], d_pods[i]) for binds / deletions made by others,
+ * or to undo a bind that failed (anchor/schedule.go:200-237).  node_idx is local to this rank. */
+int ksched_apply_delta(ksched_ctx *ctx, int64_t k, const int32_t *node_idx, const int64_t *d_cpu,
+                       const int64_t *d_mem, const int64_t *d_pods);
+/* Copies the current (local) node state back to the host. */
+int ksched_read_nodes(ksched_ctx *ctx, int64_t n, int64_t *alloc_cpu, int64_t *alloc_mem, int64_t *alloc_pods);
+/* Device-side snapshot / restore of the node state (bench: identical start state every step). */
+int ksched_save_state(ksched_ctx *ctx);
+int ksched_restore_state(ksched_ctx *ctx);
+
+/* ---- scheduling: schedulePods over p pending pods, in order (anchor/schedule.go:185-197) ----
+ * req_pods is the container count (anchor/predicate.go:78); each placed pod commits
+ * alloc[node] -= (req_cpu, req_mem, 1) (anchor/predicate.go:102).  Outputs per pod:
+ *   out_idx      node index (global across ranks) | KSCHED_NO_FIT | KSCHED_NO_POSITIVE_SCORE
+ *   out_score    winning score (resource priority) or price (best-price); 0 when not placed
+ *   out_feasible number of nodes passing predicate() for that pod at its turn
+ * Any output pointer may be NULL. */
+int ksched_schedule(ksched_ctx *ctx, int64_t p, const int64_t *req_cpu, const int64_t *req_mem,
+                    const int64_t *req_pods, const uint64_t *selector,
+                    int32_t *out_idx, double *out_score, int32_t *out_feasible);
+
+/* Same, in two halves, with the pods staged in HBM: upload once, run many times (bench). */
+int ksched_upload_pods(ksched_ctx *ctx, int64_t p, const int64_t *req_cpu, const int64_t *req_mem,
+                       const int64_t *req_pods, const uint64_t *selector);
+int ksched_run(ksched_ctx *ctx);                 /* schedules the staged pods; results stay on device */
+int ksched_sync(ksched_ctx *ctx);                /* waits for the run; fills stats */
+int ksched_download_results(ksched_ctx *ctx, int64_t p, int32_t *out_idx, double *out_score, int32_t *out_feasible);
+int ksched_get_stats(const ksched_ctx *ctx, ksched_stats *out);
+
+/* ---- host packer: Go-exact Kubernetes quantity parsing ----
+ * s == NULL means the key is absent from the ResourceList.  KSCHED_E_PARSE on the reference's
+ * errFatal paths; otherwise KSCHED_OK with the reference's value (0 for unparseable floats and for
+ * memory suffixes other than Ki/Mi). */
+int ksched_parse_cpu(const char *s, int64_t *out);    /* parseCpu, anchor/predicate.go:10-24 */
+int ksched_parse_memory(const char *s, int64_t *out); /* parseMemory, anchor/predicate.go:26-44 */
+int ksched_parse_pods(const char *s, int64_t *out);   /* parsePod, anchor/predicate.go:46-53 */
+int ksched_parse_price(const char *s, float *out);    /* node price annotation (README.md:43-48), f32 */
+
+/* Packs a Kubernetes-shaped cluster into the SoA inputs above.
+ *   nodes: n names + capacity strings (cpu/mem/pods, NULL = absent)       anchor/predicate.go:56-67
+ *   bound pods: nb pods with node name, container range [cont_off[i], cont_off[i+1]) into the
+ *     container request arrays (cpu/mem strings, NULL = absent)          anchor/predicate.go:83-105
+ * Writes alloc_* (n).  KSCHED_E_UNKNOWN_NODE if a bound pod names an unknown node. */
+int ksched_pack_nodes(int64_t n, const char *const *names, const char *const *cap_cpu,
+                      const char *const *cap_mem, const char *const *cap_pods,
+                      int64_t nb, const char *const *bound_node, const int64_t *cont_off,
+                      const char *const *cont_cpu, const char *const *cont_mem,
+                      int64_t *alloc_cpu, int64_t *alloc_mem, int64_t *alloc_pods);
+/* requestedResource (anchor/predicate.go:69-81) for p pending pods (container ranges as above). */
+int ksched_pack_pods(int64_t p, const int64_t *cont_off, const char *const *cont_cpu,
+                     const char *const *cont_mem, int64_t *req_cpu, int64_t *req_mem, int64_t *req_pods);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSCHED_H */

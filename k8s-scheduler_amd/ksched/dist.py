@@ -1,0 +1,69 @@
+"""Node-sharded multi-GPU scheduling (one process per GPU).
+
+The node list is cut into contiguous shards, one per rank (global index = shard offset + local
+index, so the lowest-index tie-break is unchanged).  Every rank scores all pending pods against its
+shard; per speculative batch the ranks exchange their local top-K candidate records (with the
+candidates' snapshot node state) by ONE RCCL all-gather issued inside the engine, merge them
+identically, and replay the same ordered commit -- each rank writes back only the nodes it owns.
+torch.distributed is used only to hand the 128-byte RCCL unique id from rank 0 to the others.
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import numpy as np
+
+
+def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) of n nodes for `rank` of `world` (sizes differ by at most one)."""
+    lo = n * rank // world
+    hi = n * (rank + 1) // world
+    return lo, hi
+
+
+def env_rank() -> Tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def broadcast_bytes(payload, rank: int, src: int = 0) -> bytes:
+    """Broadcast a small bytes object from `src` over the default torch.distributed group."""
+    import torch.distributed as dist
+    obj = [payload if rank == src else None]
+    dist.broadcast_object_list(obj, src=src)
+    return obj[0]
+
+
+def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, **kw):
+    """Engine for this rank's node shard of cluster `cl`; RCCL communicator set up when world > 1."""
+    from . import _lib as L
+    from .engine import Engine
+    lo, hi = shard_range(cl.n_nodes, rank, world)
+    if mode is None:
+        mode = L.MODE_BATCHED if (world > 1 or cl.mode != "exact") else L.MODE_EXACT
+    eng = Engine(mode=mode, priority=cl.priority, domain=cl.domain, use_labels=cl.use_labels, device=device,
+                 rank=rank, nranks=world, node_offset=lo, nodes_global=cl.n_nodes, **kw)
+    eng.load_nodes(cl.alloc_cpu[lo:hi], cl.alloc_mem[lo:hi], cl.alloc_pods[lo:hi],
+                   labels=None if cl.labels is None else cl.labels[lo:hi],
+                   price=None if cl.price is None else cl.price[lo:hi])
+    if world > 1:
+        uid = Engine.unique_id() if rank == 0 else None
+        uid = broadcast_bytes(uid, rank)
+        eng.set_comm(uid)
+    return eng, (lo, hi)
+
+
+def gather_node_state(local_state, world: int):
+    """Concatenate every rank's (cpu, mem, pods) node state in rank order (torch.distributed)."""
+    import torch
+    import torch.distributed as dist
+    out = []
+    for arr in local_state:
+        t = torch.from_numpy(np.ascontiguousarray(arr, dtype=np.int64))
+        parts = [None] * world
+        dist.all_gather_object(parts, t.numpy())
+        out.append(np.concatenate(parts))
+    return tuple(out)

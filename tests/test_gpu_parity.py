@@ -1,0 +1,170 @@
+"""GPU parity: libksched (HIP, gfx950) against the CPU oracle, bit-exact.
+
+Every test goes through the C-ABI (ctypes -> libksched.so -> HIP kernels); there is no CPU fallback.
+Outputs compared: node index per pod (exact), score bits (exact: 0 ulp, stricter than the
+north_star's 1e-6 relative), feasible count per pod (exact) and the final node state (exact).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+MODES = None
+
+
+def modes():
+    from ksched import MODE_BATCHED, MODE_EXACT
+    return [("exact", MODE_EXACT, {}), ("batched_k4", MODE_BATCHED, dict(topk=4, batch=32)),
+            ("batched_k8", MODE_BATCHED, dict(topk=8, batch=64)), ("batched_k16", MODE_BATCHED, dict(topk=16, batch=128))]
+
+
+def run_engine(cl, mode, **kw):
+    from ksched import Engine
+    with Engine(mode=mode, priority=cl.priority, domain=cl.domain, use_labels=cl.use_labels, **kw) as e:
+        e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods, labels=cl.labels, price=cl.price)
+        oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+        st = e.read_nodes()
+        stats = e.stats()
+    return oi, os_, of, st, stats
+
+
+def assert_same(got, want, label=""):
+    oi, os_, of, st = got[:4]
+    wi, ws, wf, wst = want[:4]
+    bad = np.nonzero(oi != wi)[0]
+    assert bad.size == 0, f"{label}: first idx mismatch at pod {bad[:5]}: got {oi[bad[:5]]} want {wi[bad[:5]]}"
+    sb = np.nonzero(os_.view(np.int64) != ws.view(np.int64))[0]
+    assert sb.size == 0, f"{label}: score bits differ at {sb[:5]}: {os_[sb[:5]]} vs {ws[sb[:5]]}"
+    fb = np.nonzero(of != wf)[0]
+    assert fb.size == 0, f"{label}: feasible count differs at {fb[:5]}: {of[fb[:5]]} vs {wf[fb[:5]]}"
+    for a, b in zip(st, wst):
+        assert np.array_equal(a, b), f"{label}: final node state differs"
+
+
+def golden():
+    with open(os.path.join(GOLDEN, "clusters.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("mi", range(4), ids=["exact", "b4", "b8", "b16"])
+def test_golden_clusters(gpu_available, mi):
+    from test_oracle import _cluster_from
+    name, mode, kw = modes()[mi]
+    for fx in golden():
+        cl = _cluster_from(fx)
+        got = run_engine(cl, mode, **kw)
+        want = (np.array(fx["expect_idx"], np.int32),
+                np.array([float.fromhex(x) for x in fx["expect_score_hex"]], np.float64),
+                np.array(fx["expect_feasible"], np.int32), [np.array(x, np.int64) for x in fx["expect_final"]])
+        assert_same(got, want, f"{fx['name']}/{name}")
+
+
+def test_readme_demo_best_price(gpu_available):
+    from ksched import MODE_EXACT, cluster
+    cl = cluster.readme_demo()
+    oi, os_, of, _, _ = run_engine(cl, MODE_EXACT)
+    assert oi.tolist() == [3] and os_[0] == np.float32(0.05) and of.tolist() == [6]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_edge_clusters_all_modes(gpu_available, oracle_mod, seed):
+    from ksched import cluster
+    combos = [(0, 0, False), (0, 1, False), (1, 1, False), (0, 1, True), (1, 1, True), (0, 0, True)]
+    pr, dm, lb = combos[seed % 6]
+    cl = cluster.random_small(500 + seed, n_nodes=37 + 61 * seed, n_pods=700, priority=pr, domain=dm, use_labels=lb)
+    want = oracle_mod.schedule(cl)
+    for name, mode, kw in modes():
+        assert_same(run_engine(cl, mode, **kw), want, f"seed{seed}/{name}")
+
+
+@pytest.mark.parametrize("name,nn,pp", [("c2", 5000, 2000), ("c3", 20000, 1500), ("c5", 30000, 1500)])
+def test_config_prefix_parity(gpu_available, oracle_mod, name, nn, pp):
+    from ksched import cluster
+    cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    for mname, mode, kw in modes():
+        assert_same(run_engine(cl, mode, **kw), want, f"{name}/{mname}")
+
+
+def test_exact_mode_workgroup_counts(gpu_available, oracle_mod):
+    """Exact mode with 1..many workgroups (cross-workgroup granule exchange) gives identical results."""
+    from ksched import MODE_EXACT, cluster
+    cl = cluster.make_cluster("c3", n_nodes=6000, n_pods=600)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    for g in (1, 2, 3, 7, 24, 64, 200):
+        if 6000 > g * 256 * 16:
+            continue
+        assert_same(run_engine(cl, MODE_EXACT, exact_wgs=g), want, f"G={g}")
+
+
+def test_apply_delta_and_state_roundtrip(gpu_available, oracle_mod):
+    from ksched import Engine, MODE_EXACT, cluster
+    cl = cluster.make_cluster("c3", n_nodes=2000, n_pods=300)
+    with Engine(mode=MODE_EXACT, priority=cl.priority, domain=cl.domain) as e:
+        e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods)
+        e.save_state()
+        idx = np.array([5, 7, 5, 1999], np.int32)
+        d = np.array([100, -50, 25, 1 << 40], np.int64)
+        e.apply_delta(idx, d, d * 3, -np.ones(4, np.int64))
+        ac, am, ap = e.read_nodes()
+        exp_c = cl.alloc_cpu.copy(); exp_m = cl.alloc_mem.copy(); exp_p = cl.alloc_pods.copy()
+        for i, x in zip(idx, d):
+            exp_c[i] += x; exp_m[i] += 3 * x; exp_p[i] -= 1
+        assert np.array_equal(ac, exp_c) and np.array_equal(am, exp_m) and np.array_equal(ap, exp_p)
+        e.restore_state()
+        ac, am, ap = e.read_nodes()
+        assert np.array_equal(ac, cl.alloc_cpu)
+        got1 = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods)
+        e.restore_state()
+        got2 = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods)
+        want = oracle_mod.schedule(cl)
+        for g in (got1, got2):
+            assert np.array_equal(g[0], want[0]) and np.array_equal(g[1].view(np.int64), want[1].view(np.int64))
+
+
+def test_host_mirror_fake_cluster(gpu_available, oracle_mod):
+    """schedulePods through the k8s-shaped mirror: packing, engine, ordered binds."""
+    from ksched import cluster
+    from ksched.host import Container, FakeCluster, FitError, Node, Pod
+    cl = cluster.make_cluster("c3", n_nodes=200, n_pods=400, with_strings=True)
+    nodes = [Node(nm, cap) for nm, cap in zip(cl.node_names, cl.node_capacity)]
+    bound = [Pod(f"b{i}", [Container(requests=r) for r in conts], node_name=nm)
+             for i, (nm, conts) in enumerate(cl.bound_pods)]
+    pend = [Pod(f"p{i}", [Container(requests=r) for r in conts]) for i, conts in enumerate(cl.pending_pods)]
+    fc = FakeCluster(nodes, bound + pend, priority=cl.priority, domain=cl.domain)
+    res = fc.schedule_pods()
+    want = oracle_mod.schedule(cl)
+    for (pod, r), wi in zip(res, want[0]):
+        if wi >= 0:
+            assert r.name == cl.node_names[wi] and pod.node_name == r.name
+        else:
+            assert isinstance(r, Exception)
+    # a pod that fits nowhere raises the reference's fit error
+    huge = Pod("huge", [Container(requests=dict(cpu="100000000m"))])
+    with pytest.raises(FitError):
+        fc.schedule_pod(huge)
+
+
+def test_full_size_c3_batched_equals_exact(gpu_available):
+    """Size-independent property at BASELINE size (100k pods x 50k nodes): the two independent GPU
+    paths (persistent exact kernel vs speculative batched kernels) agree bit for bit, and the final
+    node state equals the initial state minus the committed requests (conservation)."""
+    from ksched import MODE_BATCHED, MODE_EXACT, cluster
+    cl = cluster.make_cluster("c3")
+    a = run_engine(cl, MODE_EXACT)
+    b = run_engine(cl, MODE_BATCHED, topk=16, batch=128)
+    assert_same(b, a[:4], "c3 full exact-vs-batched")
+    oi = a[0]
+    placed = oi >= 0
+    exp_c = cl.alloc_cpu.copy(); exp_m = cl.alloc_mem.copy(); exp_p = cl.alloc_pods.copy()
+    np.subtract.at(exp_c, oi[placed], cl.req_cpu[placed])
+    np.subtract.at(exp_m, oi[placed], cl.req_mem[placed])
+    np.subtract.at(exp_p, oi[placed], 1)
+    assert np.array_equal(a[3][0], exp_c) and np.array_equal(a[3][1], exp_m) and np.array_equal(a[3][2], exp_p)
+    # the committed pods' recorded scores are positive (only s > 0 can win)
+    assert (a[1][placed] > 0).all()
