@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline bench: pod-node evaluations/s of the scheduling hot path (BASELINE.json metric).
+
+A step = schedulePods over the whole pending set of the workload from the same initial cluster state:
+every pod resolved in order with its placement committed before the next pod is evaluated
+(anchor/schedule.go:185-197).  The node state is restored on device at the start of each step; pods
+and nodes are HBM-resident before the timed region.  value = P x N / time (every pair the sequential
+semantics evaluates), summed over the whole job.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4] [--mode batched|exact]
+  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "k8s-scheduler_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
+BYTES_PER_PAIR = 24          # node alloc cpu/mem/pods int64 re-read per pod (sequential semantics)
+FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-score pair
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--mode", default="batched", choices=["batched", "exact"])
+    ap.add_argument("--pods", type=int, default=None)
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--topk", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--cpu-baseline-s", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check", action="store_true", help="verify a prefix against the CPU oracle")
+    return ap.parse_args()
+
+
+def cpu_baseline(cl, budget_s):
+    """The oracle's sequential C restatement (single thread, -O2 -ffp-contract=off), timed on this host
+    on a bounded prefix of the same workload: the first p pods at full node count (per-pod cost is
+    constant in the pod index)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.lib()
+    p = 16
+    t = 0.0
+    while True:
+        t0 = time.perf_counter()
+        O.schedule(cl, nthreads=1, n_pods=p)
+        t = time.perf_counter() - t0
+        if t > budget_s / 4 or p >= cl.n_pods:
+            break
+        p = min(cl.n_pods, int(p * max(2.0, budget_s / 3 / max(t, 1e-3))))
+    rate = p * cl.n_nodes / t
+    mt = None
+    try:
+        nthr = os.cpu_count() or 1
+        nthr = min(nthr, 16)
+        pm = max(16, min(cl.n_pods, int(p * 2)))
+        t0 = time.perf_counter()
+        O.schedule(cl, nthreads=nthr, n_pods=pm)
+        tm = time.perf_counter() - t0
+        mt = dict(value=pm * cl.n_nodes / tm, unit="pod-node evals/s", cores=nthr, kind="port",
+                  sample=f"first {pm} pods of {cl.name} at {cl.n_nodes} nodes, OpenMP node-parallel, one barrier per pod")
+    except Exception:
+        pass
+    return dict(value=rate, unit="pod-node evals/s", cores=1, kind="port",
+                sample=f"first {p} pods of {cl.name} at full {cl.n_nodes} nodes, sequential commit, 1 thread "
+                       f"({t:.1f} s; Go reference unbuildable here: no Go toolchain)"), mt
+
+
+def main():
+    args = parse()
+    from ksched import MODE_BATCHED, MODE_EXACT, cluster
+    from ksched.dist import env_rank, make_sharded_engine
+    rank, world, local = env_rank()
+    world = max(world, 1)
+    if world != args.gpus and args.gpus > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import torch
+
+    cl = cluster.make_cluster(args.config, n_nodes=args.nodes, n_pods=args.pods)
+    mode = MODE_EXACT if args.mode == "exact" else MODE_BATCHED
+    if world > 1 and mode == MODE_EXACT:
+        mode = MODE_BATCHED
+    eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=local, mode=mode, topk=args.topk,
+                                        batch=args.batch, timing=True)
+    eng.save_state()
+    eng.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+
+    def step():
+        eng.restore_state()
+        eng.run()
+        eng.sync()
+
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kstats = []
+    for _ in range(args.steps):
+        step()
+        kstats.append(eng.stats())
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed * 1000.0 / args.steps
+    pairs = cl.n_pods * cl.n_nodes
+    value = pairs * args.steps / elapsed
+    st = kstats[-1]
+    # dominant kernel family by timed device time (sampled batches)
+    names = ["k_exact" if mode == MODE_EXACT else "k_score_topk", "k_merge", "k_commit", "rccl_allgather+merge"]
+    fam_ms = [sum(s["kernel_ms"][f] for s in kstats) for f in range(4)]
+    fam_n = [sum(s["kernel_launches"][f] for s in kstats) for f in range(4)]
+    dom = int(np.argmax([fam_ms[f] / max(fam_n[f], 1) * (st["batches"] if mode == MODE_BATCHED else 1) for f in range(4)]))
+    score_pairs = sum(s["kernel_pairs"][0] for s in kstats)
+    score_avg_ms = fam_ms[0] / max(fam_n[0], 1)
+    score_pairs_per_launch = score_pairs / max(fam_n[0], 1)
+    achieved_gbs = score_pairs_per_launch * BYTES_PER_PAIR / (score_avg_ms * 1e-3) / 1e9 if score_avg_ms > 0 else 0.0
+    fam_share = {names[f]: (fam_ms[f] / max(fam_n[f], 1)) for f in range(4)}
+    placed = int(st["placed"])
+    out = {
+        "metric": "pod-node evaluations/sec",
+        "value": value,
+        "unit": "pod-node evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"{args.config}: {cl.n_pods} pending pods x {cl.n_nodes} nodes, "
+                               f"{'resource (balanced+least-requested)' if cl.priority == 0 else 'best-price'} priority, "
+                               f"{'feasible-only' if cl.domain else 'all-node'} argmax, labels={bool(cl.use_labels)}",
+                   "nodes": cl.n_nodes, "pods": cl.n_pods, "mode": args.mode, "topk": args.topk,
+                   "batch": int(eng.opts.batch) or 8 * args.topk, "parallelism": f"node-shard x{world}"},
+        "pods_per_sec": cl.n_pods * args.steps / elapsed,
+        "placed_pods": placed,
+        "batches_per_step": int(st["batches"]),
+        "truncated_batches_per_step": int(st["truncations"]),
+        "kernel_avg_ms": fam_share,
+        "roofline": {
+            "kernel": names[0],
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": None,
+            "algorithmic_bytes_per_pair": BYTES_PER_PAIR,
+            "pairs_per_launch": score_pairs_per_launch,
+            "avg_launch_ms": score_avg_ms,
+            "fp64_tflops_equiv": score_pairs_per_launch * FLOPS_PER_PAIR / (score_avg_ms * 1e-3) / 1e12 if score_avg_ms > 0 else 0.0,
+            "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
+            "dominant_family": names[dom],
+        },
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        base, mt = cpu_baseline(cl, args.cpu_baseline_s)
+        out["cpu_baseline"] = base
+        if mt:
+            out["cpu_baseline_mt"] = mt
+    if args.check and rank == 0 and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        oi, os_, of = eng.results()
+        k = min(cl.n_pods, 2000)
+        wi, ws, wf, _ = O.schedule(cl, nthreads=8, n_pods=k)
+        out["check_prefix_pods"] = k
+        out["check_ok"] = bool(np.array_equal(oi[:k], wi) and np.array_equal(os_[:k].view(np.int64), ws.view(np.int64)))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

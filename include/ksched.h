@@ -66,7 +66,9 @@ typedef struct ksched_opts {
     int64_t node_offset;  /* global index of this rank's first node */
     int64_t nodes_global; /* total nodes across ranks (0 = local count when nranks == 1) */
     int32_t exact_wgs;    /* exact mode: workgroups (0 = auto) */
-    int32_t reserved[7];
+    int32_t timing;       /* 1: time kernel families with HIP events on the engine stream (sampled) */
+    int32_t timing_every; /* batched mode: time one batch in every N (0 = 16) */
+    int32_t reserved[5];
 } ksched_opts;
 
 typedef struct ksched_ctx ksched_ctx;
@@ -78,8 +80,10 @@ typedef struct ksched_stats {
     int64_t truncations;   /* batches cut short by a candidate-list overflow */
     int64_t pair_evals;    /* pod-node pairs evaluated by the score kernels */
     double device_ms;      /* device time of the last schedule call (HIP events) */
-    double kernel_ms[4];   /* per kernel family: [0] score/exact, [1] merge, [2] commit, [3] collective */
-    int64_t kernel_launches[4];
+    double kernel_ms[4];   /* timed device ms per kernel family: [0] score (or the exact kernel),
+                              [1] merge, [2] commit, [3] collective (all-gather + rank merge) */
+    int64_t kernel_launches[4]; /* number of timed batches (launch groups) behind kernel_ms */
+    int64_t kernel_pairs[4];    /* pod-node pairs evaluated by the timed family-0 launches */
 } ksched_stats;
 
 /* ---- lifecycle ---- */

@@ -54,6 +54,10 @@ struct ksched_ctx {
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool running = false;
+    std::vector<hipEvent_t> ev_pool;  // sampled per-family event pairs (opts.timing)
+    struct Timed { int fam; int e0, e1; int64_t pairs; };
+    std::vector<Timed> timed;
+    size_t ev_used = 0;
     ksched_stats st{};
     int64_t run_batches = 0;
 };
@@ -92,6 +96,35 @@ hipError_t grow(T **ptr, int64_t *cap, int64_t need, size_t elem) {
 int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return v && *v ? std::atoi(v) : dflt;
+}
+
+// Sampled kernel timing: a (start, stop) event pair around one kernel family of one batch.
+hipError_t ev_take(ksched_ctx *c, int *idx) {
+    if (c->ev_used >= c->ev_pool.size()) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        c->ev_pool.push_back(e);
+    }
+    *idx = (int)c->ev_used++;
+    return hipSuccess;
+}
+
+hipError_t ev_begin(ksched_ctx *c, bool on, int *e0) {
+    if (!on) return hipSuccess;
+    hipError_t r = ev_take(c, e0);
+    if (r != hipSuccess) return r;
+    return hipEventRecord(c->ev_pool[(size_t)*e0], c->stream);
+}
+
+hipError_t ev_end(ksched_ctx *c, bool on, int fam, int e0, int64_t pairs) {
+    if (!on) return hipSuccess;
+    int e1;
+    hipError_t r = ev_take(c, &e1);
+    if (r != hipSuccess) return r;
+    r = hipEventRecord(c->ev_pool[(size_t)e1], c->stream);
+    if (r == hipSuccess) c->timed.push_back({fam, e0, e1, pairs});
+    return r;
 }
 
 // Batched-mode geometry for one schedule call.
@@ -178,17 +211,18 @@ int enqueue_batched(ksched_ctx *c) {
         int64_t m = (int64_t)std::ceil((double)(c->p - resolved) / avg_progress);
         m = std::max<int64_t>(1, std::min<int64_t>(m, poll > 0 ? poll : 256));
         for (int64_t it = 0; it < m; ++it) {
+            const bool tm = c->o.timing && (batches % (c->o.timing_every > 0 ? c->o.timing_every : 16) == 0);
+            int e0 = -1;
             ScoreArgs sa{};
             sa.nodes = c->d_nodes; sa.n_local = c->n_local; sa.node_offset = c->o.node_offset;
             sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = c->d_cursor; sa.B = pl.B;
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part);
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt);
-            if (c->n_local > 0) {
-                HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, sa, pl.pod_groups, c->stream));
-            } else {
-                // empty shard: one empty chunk (the kernel writes empty lists and zero counts)
-                HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, sa, pl.pod_groups, c->stream));
-            }
+            // (an empty shard runs one empty chunk: the kernel writes empty lists and zero counts)
+            HIPCHK(c, ev_begin(c, tm, &e0));
+            HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, sa, pl.pod_groups, c->stream));
+            HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local));
+            HIPCHK(c, ev_begin(c, tm, &e0));
             // merge stages
             const void *in = sa.part;
             const int64_t *in_cnt = sa.part_cnt;
@@ -211,9 +245,11 @@ int enqueue_batched(ksched_ctx *c) {
                 HIPCHK(c, launch_merge(pl.K, false, fin, ma, c->stream));
                 in = ma.out; in_cnt = ma.out_cnt;
             }
+            HIPCHK(c, ev_end(c, tm, 1, e0, 0));
             const Rec *lists = reinterpret_cast<const Rec *>(ws + pl.off_lists);
             const int64_t *fc0 = reinterpret_cast<const int64_t *>(ws + pl.off_fc);
             if (R > 1) {
+                HIPCHK(c, ev_begin(c, tm, &e0));
                 NCCLCHK(c, ncclAllGather(ws + pl.off_send, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, c->stream));
                 MergeArgs ma{};
                 ma.in = ws + pl.off_recv; ma.rank_stride = (int64_t)pl.send_bytes; ma.C_in = R; ma.C_out = 1;
@@ -223,6 +259,7 @@ int enqueue_batched(ksched_ctx *c) {
                 HIPCHK(c, launch_merge(pl.K, true, true, ma, c->stream));
                 lists = ma.out_rec;
                 fc0 = ma.out_fc;
+                HIPCHK(c, ev_end(c, tm, 3, e0, 0));
             }
             CommitArgs ca{};
             ca.lists = lists; ca.fc0 = fc0; ca.pods = pods; ca.cursor = c->d_cursor; ca.B = pl.B;
@@ -230,7 +267,9 @@ int enqueue_batched(ksched_ctx *c) {
             ca.n_global = c->n_global; ca.bitmap_words = words;
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.stats = c->d_cursor + 1;
+            HIPCHK(c, ev_begin(c, tm, &e0));
             HIPCHK(c, launch_commit(pl.K, prio, dom, lab, ca, (size_t)lds, c->stream));
+            HIPCHK(c, ev_end(c, tm, 2, e0, 0));
             ++batches;
         }
         HIPCHK(c, hipMemcpyAsync(c->h_cursor, c->d_cursor, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
@@ -277,7 +316,10 @@ int enqueue_exact(ksched_ctx *c) {
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     a.slots = c->d_slots; a.err = c->d_err;
     a.timeout_ticks = (int64_t)env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000) * 100000;  // 100 MHz wall clock
+    int e0 = -1;
+    HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0));
     HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, a, kExactBlock, G > 1, c->stream));
+    HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n));
     c->st.pair_evals = c->p * n;
     c->st.batches = 0;
     c->st.truncations = 0;
@@ -348,6 +390,7 @@ int ksched_destroy(ksched_ctx *c) {
     hipFree(c->d_oidx); hipFree(c->d_osc); hipFree(c->d_ofeas);
     hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_slots); hipFree(c->d_err);
     if (c->h_cursor) hipHostFree(c->h_cursor);
+    for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -510,6 +553,8 @@ int ksched_run(ksched_ctx *c) {
     HIPCHK(c, hipSetDevice(c->dev));
     c->err.clear();
     c->st = ksched_stats{};
+    c->timed.clear();
+    c->ev_used = 0;
     c->st.pods = c->p;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int r = KSCHED_OK;
@@ -532,6 +577,14 @@ int ksched_sync(ksched_ctx *c) {
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
         c->st.device_ms = ms;
         c->running = false;
+        for (const auto &t : c->timed) {
+            float km = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&km, c->ev_pool[(size_t)t.e0], c->ev_pool[(size_t)t.e1]));
+            c->st.kernel_ms[t.fam] += km;
+            c->st.kernel_launches[t.fam] += 1;
+            c->st.kernel_pairs[t.fam] += t.pairs;
+        }
+        c->timed.clear();
     }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));

@@ -35,13 +35,13 @@ class Opts(C.Structure):
                 ("domain", C.c_int32), ("use_labels", C.c_int32), ("batch", C.c_int32), ("topk", C.c_int32),
                 ("device", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32),
                 ("node_offset", C.c_int64), ("nodes_global", C.c_int64), ("exact_wgs", C.c_int32),
-                ("reserved", C.c_int32 * 7)]
+                ("timing", C.c_int32), ("timing_every", C.c_int32), ("reserved", C.c_int32 * 5)]
 
 
 class Stats(C.Structure):
     _fields_ = [("pods", C.c_int64), ("placed", C.c_int64), ("batches", C.c_int64), ("truncations", C.c_int64),
                 ("pair_evals", C.c_int64), ("device_ms", C.c_double), ("kernel_ms", C.c_double * 4),
-                ("kernel_launches", C.c_int64 * 4)]
+                ("kernel_launches", C.c_int64 * 4), ("kernel_pairs", C.c_int64 * 4)]
 
 
 class KschedError(RuntimeError):

@@ -25,13 +25,15 @@ def _i64(a):
 class Engine:
     def __init__(self, mode: int = L.MODE_AUTO, priority: int = L.PRIORITY_RESOURCE, domain: int = L.DOMAIN_ALL,
                  use_labels: bool = False, batch: int = 0, topk: int = 0, device: int = -1,
-                 rank: int = 0, nranks: int = 1, node_offset: int = 0, nodes_global: int = 0, exact_wgs: int = 0):
+                 rank: int = 0, nranks: int = 1, node_offset: int = 0, nodes_global: int = 0, exact_wgs: int = 0,
+                 timing: bool = False, timing_every: int = 0):
         lb = L.lib()
         o = L.Opts()
         L.check(lb.ksched_default_opts(C.byref(o)), what="default_opts")
         o.mode, o.priority, o.domain, o.use_labels = mode, priority, domain, int(bool(use_labels))
         o.batch, o.topk, o.device = batch, topk, device
         o.rank, o.nranks, o.node_offset, o.nodes_global, o.exact_wgs = rank, nranks, node_offset, nodes_global, exact_wgs
+        o.timing, o.timing_every = int(bool(timing)), timing_every
         ctx = L.CTX()
         L.check(lb.ksched_create(C.byref(o), C.byref(ctx)), what="create")
         self._ctx = ctx
@@ -126,7 +128,8 @@ class Engine:
         s = L.Stats()
         self._chk(L.lib().ksched_get_stats(self._ctx, C.byref(s)), "get_stats")
         return dict(pods=s.pods, placed=s.placed, batches=s.batches, truncations=s.truncations,
-                    pair_evals=s.pair_evals, device_ms=s.device_ms)
+                    pair_evals=s.pair_evals, device_ms=s.device_ms, kernel_ms=list(s.kernel_ms),
+                    kernel_launches=list(s.kernel_launches), kernel_pairs=list(s.kernel_pairs))
 
     def schedule(self, req_cpu, req_mem, req_pods, selector=None):
         """schedulePods over the given pending pods (in order).  Returns (idx, score, feasible)."""
