@@ -181,7 +181,7 @@ BatchPlan plan_batch(const ksched_ctx *c) {
 int64_t commit_lds_bytes(const ksched_ctx *c, int B, int *words) {
     const int64_t w = (c->n_global + 31) / 32;
     *words = (int)align_up((size_t)w, 4);
-    return (int64_t)*words * 4 + (int64_t)B * (int64_t)sizeof(Touched);
+    return (int64_t)*words * 4 + (int64_t)B * (int64_t)(sizeof(Touched) + kPodStageBytes);
 }
 
 int enqueue_batched(ksched_ctx *c) {
@@ -207,6 +207,7 @@ int enqueue_batched(ksched_ctx *c) {
     int64_t resolved = 0, batches = 0;
     double avg_progress = std::max(1.0, pl.K * 2.0);
     const int poll = env_int("KSCHED_POLL_BATCHES", 0);
+    const bool single_wave = env_int("KSCHED_COMMIT_WAVES", 1) == 1;
     while (resolved < c->p) {
         int64_t m = (int64_t)std::ceil((double)(c->p - resolved) / avg_progress);
         m = std::max<int64_t>(1, std::min<int64_t>(m, poll > 0 ? poll : 256));
@@ -268,7 +269,7 @@ int enqueue_batched(ksched_ctx *c) {
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.stats = c->d_cursor + 1;
             HIPCHK(c, ev_begin(c, tm, &e0));
-            HIPCHK(c, launch_commit(pl.K, prio, dom, lab, ca, (size_t)lds, c->stream));
+            HIPCHK(c, launch_commit(pl.K, prio, dom, lab, ca, (size_t)lds, single_wave, c->stream));
             HIPCHK(c, ev_end(c, tm, 2, e0, 0));
             ++batches;
         }

@@ -101,7 +101,9 @@ hipError_t launch_exact(int npt, int prio, int dom, bool lab, const ExactArgs &a
                         hipStream_t s);
 hipError_t launch_score_topk(int K, int prio, int dom, bool lab, const ScoreArgs &a, int pod_groups, hipStream_t s);
 hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
-hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, hipStream_t s);
+hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, bool single_wave,
+                         hipStream_t s);
+constexpr size_t kPodStageBytes = 40;  // LDS per batch pod staged by the single-wave commit
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
 

@@ -456,6 +456,148 @@ __global__ __launch_bounds__(kCommitBlock) void k_commit(CommitArgs A) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Ordered commit, single-wave sequencer (the default).  Same decision rule as k_commit, but:
+//   - one wave, no barriers: every per-pod reduction is a wave butterfly and every lane evaluates the
+//     (wave-uniform) decision itself; the touched table and node bitmap live in LDS;
+//   - the batch's requests and feasible counts are staged into LDS once, up front;
+//   - lane q < K holds candidate q of the current pod and already has the NEXT pod's candidate load
+//     in flight (software prefetch), so no dependent global load sits on the serial path.
+// ------------------------------------------------------------------------------------------------
+struct alignas(8) PodStage {
+    int64_t rc, rm, rp;
+    uint64_t sel;
+    int64_t fc0;
+};
+
+template <int K, int PRIO, int DOM, bool LAB>
+__global__ __launch_bounds__(64) void k_commit1(CommitArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint32_t *bitmap = reinterpret_cast<uint32_t *>(smem);
+    Touched *T = reinterpret_cast<Touched *>(smem + (size_t)A.bitmap_words * 4);
+    PodStage *PS = reinterpret_cast<PodStage *>(smem + (size_t)A.bitmap_words * 4 + (size_t)A.B * sizeof(Touched));
+    const int lane = threadIdx.x;
+    const int64_t p0 = *A.cursor;
+    if (p0 >= A.pods.p) return;
+    const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);
+    for (int w = lane; w < A.bitmap_words; w += 64) bitmap[w] = 0;
+    for (int b = lane; b < nb; b += 64) {
+        PodStage s;
+        s.rc = A.pods.rc[p0 + b]; s.rm = A.pods.rm[p0 + b]; s.rp = A.pods.rp[p0 + b];
+        s.sel = LAB ? A.pods.sel[p0 + b] : 0;
+        s.fc0 = A.fc0[b];
+        PS[b] = s;
+    }
+    Rec nxt;
+    if (lane < K) nxt = A.lists[lane];
+    else { nxt.valid = 0; nxt.idx = kNoIdx; nxt.key = -__builtin_inf(); }
+    __syncthreads();  // one wave: orders the staging writes before the loop's reads
+
+    int nT = 0;
+    int done = nb;
+    int64_t placed = 0;
+    for (int i = 0; i < nb; ++i) {
+        const Rec my = nxt;
+        if (lane < K && i + 1 < nb) nxt = A.lists[(size_t)(i + 1) * K + lane];
+        const PodStage ps = PS[i];
+        const int64_t rc = ps.rc, rm = ps.rm, rp = ps.rp;
+        const uint64_t sel = ps.sel;
+        const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+        // re-score the nodes already committed in this batch
+        int64_t df = 0;
+        double tk = -__builtin_inf();
+        int32_t ti = kNoIdx, ts = -1;
+        for (int t = lane; t < nT; t += 64) {
+            const Touched &x = T[t];
+            const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
+            const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
+            df += (int64_t)f1 - (int64_t)f0;
+            double k;
+            if (pair_key<PRIO, DOM>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2], (double)x.cur[0],
+                                    (double)x.cur[1], (double)x.cur[2], x.price, &k) &&
+                better(k, x.idx, tk, ti)) {
+                tk = k; ti = x.idx; ts = t;
+            }
+        }
+        // candidate list: valid prefix, first entry not committed in this batch
+        const bool valid = lane < K && my.valid;
+        const bool untouched = valid && !(bitmap[(uint32_t)my.idx >> 5] & (1u << ((uint32_t)my.idx & 31)));
+        const uint64_t vmask = __ballot(valid);
+        const uint64_t umask = __ballot(untouched);
+        const int cv = __popcll(vmask);
+        const int uq = umask ? __ffsll((unsigned long long)umask) - 1 : K;
+        wave_argbest(tk, ti, ts);
+        df = wave_sum_i64(df);
+        const int64_t fc = ps.fc0 + df;
+        int32_t oidx = -1;
+        double osc = 0.0;
+        int kind = 0;  // 0 none, 1 winner from list (new touch), 2 winner already touched, 3 overflow
+        double wk = 0.0;
+        int32_t wi = kNoIdx;
+        if (fc != 0) {
+            if (uq < cv) {
+                const double uk = __shfl(my.key, uq, 64);
+                const int32_t ui = __shfl(my.idx, uq, 64);
+                if (ti != kNoIdx && better(tk, ti, uk, ui)) { kind = 2; wk = tk; wi = ti; }
+                else { kind = 1; wk = uk; wi = ui; }
+            } else if (cv < K) {
+                if (ti != kNoIdx) { kind = 2; wk = tk; wi = ti; }
+            } else {
+                const double lk = __shfl(my.key, K - 1, 64);
+                const int32_t li = __shfl(my.idx, K - 1, 64);
+                if (ti != kNoIdx && better(tk, ti, lk, li)) { kind = 2; wk = tk; wi = ti; }
+                else kind = 3;
+            }
+        }
+        if (kind == 3) { done = i; break; }  // wave-uniform
+        if (fc != 0) {
+            if (kind == 0) {
+                oidx = -2;
+            } else {
+                oidx = wi;
+                osc = PRIO == kPrioPrice ? -wk : wk;
+                ++placed;
+                if (kind == 1) {
+                    if (lane == uq) {  // first touch: the holder of the candidate opens the slot
+                        Touched &x = T[nT];
+                        x.idx = my.idx; x.pad = 0;
+                        x.s0[0] = my.a[0]; x.s0[1] = my.a[1]; x.s0[2] = my.a[2];
+                        x.cur[0] = wsub(my.a[0], rc); x.cur[1] = wsub(my.a[1], rm); x.cur[2] = wsub(my.a[2], 1);
+                        x.labels = my.labels; x.price = my.price; x.pad2 = 0;
+                        bitmap[(uint32_t)my.idx >> 5] |= 1u << ((uint32_t)my.idx & 31);
+                    }
+                    ++nT;
+                } else if (lane == 0) {
+                    Touched &x = T[ts];
+                    x.cur[0] = wsub(x.cur[0], rc); x.cur[1] = wsub(x.cur[1], rm); x.cur[2] = wsub(x.cur[2], 1);
+                }
+            }
+        }
+        if (lane == 0) {
+            const int64_t pod = p0 + i;
+            A.out.idx[pod] = oidx;
+            A.out.score[pod] = osc;
+            A.out.feas[pod] = (int32_t)fc;
+        }
+    }
+    __syncthreads();
+    for (int t = lane; t < nT; t += 64) {
+        const Touched &x = T[t];
+        const int64_t j = (int64_t)x.idx - A.node_lo;
+        if (j >= 0 && j < A.n_local) {
+            NodeRec *nd = A.nodes + j;
+            nd->a[0] = x.cur[0]; nd->a[1] = x.cur[1]; nd->a[2] = x.cur[2];
+            nd->af[0] = (double)x.cur[0]; nd->af[1] = (double)x.cur[1]; nd->af[2] = (double)x.cur[2];
+        }
+    }
+    if (lane == 0) {
+        *A.cursor = p0 + done;
+        A.stats[0] += 1;
+        A.stats[1] += (done < nb) ? 1 : 0;
+        A.stats[2] += placed;
+    }
+}
+
 __global__ void k_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d) {
     // Sequential in one lane: deltas may repeat a node and must apply in order (wrapping adds).
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -531,24 +673,25 @@ hipError_t merge_k(bool rec, bool fin, const MergeArgs &a, hipStream_t s) {
 }
 
 template <int K, int PRIO, int DOM, bool LAB>
-hipError_t commit_one(const CommitArgs &a, size_t lds, hipStream_t s) {
-    auto fn = k_commit<K, PRIO, DOM, LAB>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+hipError_t commit_one(const CommitArgs &a, size_t lds, bool single_wave, hipStream_t s) {
+    static bool attr_set[2] = {false, false};
+    const void *fn = single_wave ? (const void *)k_commit1<K, PRIO, DOM, LAB> : (const void *)k_commit<K, PRIO, DOM, LAB>;
+    if (!attr_set[single_wave]) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_set[single_wave] = true;
     }
-    hipLaunchKernelGGL(fn, dim3(1), dim3(kCommitBlock), lds, s, a);
+    if (single_wave) hipLaunchKernelGGL((k_commit1<K, PRIO, DOM, LAB>), dim3(1), dim3(64), lds, s, a);
+    else hipLaunchKernelGGL((k_commit<K, PRIO, DOM, LAB>), dim3(1), dim3(kCommitBlock), lds, s, a);
     return hipGetLastError();
 }
 
 template <int PRIO, int DOM, bool LAB>
-hipError_t commit_k(int K, const CommitArgs &a, size_t lds, hipStream_t s) {
+hipError_t commit_k(int K, const CommitArgs &a, size_t lds, bool sw, hipStream_t s) {
     switch (K) {
-        case 4: return commit_one<4, PRIO, DOM, LAB>(a, lds, s);
-        case 8: return commit_one<8, PRIO, DOM, LAB>(a, lds, s);
-        case 16: return commit_one<16, PRIO, DOM, LAB>(a, lds, s);
+        case 4: return commit_one<4, PRIO, DOM, LAB>(a, lds, sw, s);
+        case 8: return commit_one<8, PRIO, DOM, LAB>(a, lds, sw, s);
+        case 16: return commit_one<16, PRIO, DOM, LAB>(a, lds, sw, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -588,8 +731,9 @@ hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs
     }
 }
 
-hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, (commit_k<P_, D_, L_>(K, a, lds_bytes, s)));
+hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, bool single_wave,
+                         hipStream_t s) {
+    KSCHED_DISPATCH(prio, dom, lab, (commit_k<P_, D_, L_>(K, a, lds_bytes, single_wave, s)));
 }
 
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
