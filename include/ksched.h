@@ -132,6 +132,12 @@ int ksched_sync(ksched_ctx *ctx);                /* waits for the run; fills sta
 int ksched_download_results(ksched_ctx *ctx, int64_t p, int32_t *out_idx, double *out_score, int32_t *out_feasible);
 int ksched_get_stats(const ksched_ctx *ctx, ksched_stats *out);
 
+/* Diagnostics: out_native[i] = a[i] / b[i] (hipcc's f64 division) and out_fast[i] = the engine's
+ * hoisted-reciprocal division of the same operands, both computed on the device (bit-exactness
+ * check of the division used by every score kernel). */
+int ksched_selftest_fastdiv(ksched_ctx *ctx, int64_t n, const double *a, const double *b, double *out_native,
+                            double *out_fast);
+
 /* ---- host packer: Go-exact Kubernetes quantity parsing ----
  * s == NULL means the key is absent from the ResourceList.  KSCHED_E_PARSE on the reference's
  * errFatal paths; otherwise KSCHED_OK with the reference's value (0 for unparseable floats and for

@@ -24,15 +24,16 @@ constexpr int kDomAll = 0;
 constexpr int kDomFeasible = 1;
 constexpr int32_t kNoIdx = 0x7fffffff;  // "no candidate" index (ranks after every real node)
 
-// Node state as kept in HBM (AoS, 64 B: one s_load_dwordx16 when wave-uniform).
+// Node state as kept in HBM (AoS, 96 B: s_load_dwordx16 + s_load_dwordx8 when wave-uniform).
 struct alignas(16) NodeRec {
     int64_t a[3];      // allocatable cpu (millicores), memory (KiB), pods = capacity - used
     uint64_t labels;   // label bitset (build extension)
-    double af[3];      // (double)a[k], kept in sync with a[k] by every writer
+    double af[3];      // (double)a[k], kept in sync with a[k] by every writer (device side)
+    double y[3];       // recip(af[k]): hipcc's refined reciprocal of the divisor (0 when a[k] == 0)
     float price;       // node price (best-price priority)
-    uint32_t pad;
+    uint32_t pad[3];
 };
-static_assert(sizeof(NodeRec) == 64, "NodeRec layout");
+static_assert(sizeof(NodeRec) == 96, "NodeRec layout");
 
 // One candidate of a partial top-K list (score kernels -> merge kernels).
 struct alignas(16) Cand {
@@ -68,6 +69,85 @@ __device__ __forceinline__ bool fits(int64_t rc, int64_t rm, int64_t rp, uint64_
     if (use_labels) f &= ((lab & sel) == sel);
     return f;
 }
+
+// ---- f64 division with a hoisted divisor reciprocal, bit-identical to hipcc's `a / b` ----------
+// hipcc lowers a double division to (gfx950 ISA, checked in DESIGN.md):
+//   d = v_div_scale(b, b, a); r = v_rcp(d); e = fma(-d, r, 1); r = fma(r, e, r);
+//   e = fma(-d, r, 1); r = fma(r, e, r);  n = v_div_scale(a, b, a); q = n * r;
+//   rm = fma(-d, q, n); q = v_div_fmas(rm, r, q); result = v_div_fixup(q, b, a)
+// For the operands of this path -- integer-valued divisors 1 <= |b| <= 2^63 or b = 3, numerators
+// that are integer-valued, or sums/squares of such quotients (|a| >= 2^-200 or a == 0) -- both
+// div_scale are identities (no exponent gap >= 768, no denormal divisor or reciprocal, numerator
+// exponent far above the 2^-970 rescale threshold), div_fmas is a plain fma (VCC = 0) and div_fixup
+// passes a finite normal quotient through.  So the refined reciprocal r depends on b alone and can
+// be computed once per divisor; the per-numerator part is 3 instructions.  Signed zeros of a zero
+// numerator may differ from the native sequence but never reach a score.
+__device__ __forceinline__ double recip(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+__device__ __forceinline__ double qdiv(double a, double b, double y) {
+    const double q = a * y;
+    const double rm = __builtin_fma(-b, q, a);
+    return __builtin_fma(rm, y, q);
+}
+
+// Resource score with hoisted reciprocals y* of the allocatable values and y3 = recip(3.0).
+// FAST53: every |alloc| and |request| < 2^52 (host-checked for the whole call), so
+// (double)(a - r) == (double)a - (double)r exactly and the int64->f64 conversion is skipped.
+template <bool FAST53>
+__device__ __forceinline__ double resource_score_fast(int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,
+                                                      double rpf, int64_t ac, int64_t am, int64_t ap, double acf,
+                                                      double amf, double apf, double yc, double ym, double yp,
+                                                      double y3) {
+    const double c = (ac == 0) ? 1.0 : qdiv(rcf, acf, yc);
+    const double m = (am == 0) ? 1.0 : qdiv(rmf, amf, ym);
+    const double p = (ap == 0) ? 1.0 : qdiv(rpf, apf, yp);
+    double b = 0.0;
+    if (!(c >= 1.0 || m >= 1.0 || p >= 1.0)) {
+        const double mean = qdiv((c + m) + p, 3.0, y3);
+        const double cr = (c - mean) * (c - mean);
+        const double mr = (m - mean) * (m - mean);
+        const double pr = (p - mean) * (p - mean);
+        const double var = qdiv((cr + mr) + pr, 3.0, y3);
+        b = (1.0 - var) * 10.0;
+    }
+    const double dc = FAST53 ? acf - rcf : (double)wsub(ac, rc);
+    const double dm = FAST53 ? amf - rmf : (double)wsub(am, rm);
+    const double dp = FAST53 ? apf - rpf : (double)wsub(ap, rp);
+    const double lc = (ac == 0 || rc > ac) ? 0.0 : qdiv(dc * 10.0, acf, yc);
+    const double lm = (am == 0 || rm > am) ? 0.0 : qdiv(dm * 10.0, amf, ym);
+    const double lp = (ap == 0 || rp > ap) ? 0.0 : qdiv(dp * 10.0, apf, yp);
+    const double l = qdiv((lc + lm) + lp, 3.0, y3);
+    double s = 0.0;
+    s += b;
+    s += l;
+    s *= 0.5;  // x / 2 == x * 0.5 exactly (both are the correctly rounded x/2)
+    return s;
+}
+
+template <int PRIO, int DOM, bool FAST53>
+__device__ __forceinline__ bool pair_key_fast(bool feas, int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,
+                                              double rpf, int64_t ac, int64_t am, int64_t ap, double acf,
+                                              double amf, double apf, double yc, double ym, double yp, double y3,
+                                              float price, double *key) {
+    if (PRIO == kPrioPrice) {
+        *key = -(double)price;
+        return feas;
+    } else {
+        if (DOM == kDomFeasible && !feas) return false;
+        const double s = resource_score_fast<FAST53>(rc, rm, rp, rcf, rmf, rpf, ac, am, ap, acf, amf, apf, yc, ym,
+                                                     yp, y3);
+        *key = s;
+        return s > 0.0;
+    }
+}
+
+__device__ __forceinline__ double recip_or_zero(int64_t a, double af) { return a == 0 ? 0.0 : recip(af); }
 
 // The resource score of one (request, allocatable) pair.  rcf/... are (double) of the int64 values
 // (hoisted by callers; (double)int64 is correctly rounded, identical wherever it is computed).
@@ -116,29 +196,92 @@ __device__ __forceinline__ bool pair_key(bool feas, int64_t rc, int64_t rm, int6
     }
 }
 
-// Wave-wide (64 lanes) arg-best of (key, idx, aux) by butterfly; every lane ends with the result.
-__device__ __forceinline__ void wave_argbest(double &key, int32_t &idx, int32_t &aux) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double ok = __shfl_xor(key, off, 64);
-        const int32_t oi = __shfl_xor(idx, off, 64);
-        const int32_t oa = __shfl_xor(aux, off, 64);
-        if (better(ok, oi, key, idx)) { key = ok; idx = oi; aux = oa; }
+// ---- register-only wave butterflies (no LDS round trip) --------------------------------------
+// Partner exchange for butterfly stage S (every lane ends with the all-reduce):
+//   S0 quad_perm[1,0,3,2]  S1 quad_perm[2,3,0,1]  S2 row_half_mirror  S3 row_mirror   (DPP)
+//   S4 v_permlane16_swap (lane ^ 16)               S5 v_permlane32_swap (lane ^ 32)   (gfx950)
+// After S0..S1 a quad holds its result in every lane; half_mirror pairs the two quads of an
+// 8-lane group, mirror the two 8-groups of a row, then rows exchange across 16 and 32.
+template <int S>
+__device__ __forceinline__ uint32_t wpartner(uint32_t v) {
+    if constexpr (S == 0) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (S == 1) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (S == 2) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false);
+    else if constexpr (S == 3) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false);
+    else if constexpr (S == 4) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // {vdst_new, vsrc_new}
+        return ((__lane_id() >> 4) & 1) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (__lane_id() >> 5) ? r[0] : r[1];
     }
 }
 
-__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+template <int S>
+__device__ __forceinline__ double wpartner_f64(double v) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint64_t hi = wpartner<S>((uint32_t)(u >> 32)), lo = wpartner<S>((uint32_t)u);
+    return __longlong_as_double((long long)((hi << 32) | lo));
+}
+
+template <int S>
+__device__ __forceinline__ void argbest_stage(double &key, int32_t &idx, int32_t &aux) {
+    const double ok = wpartner_f64<S>(key);
+    const int32_t oi = (int32_t)wpartner<S>((uint32_t)idx);
+    const int32_t oa = (int32_t)wpartner<S>((uint32_t)aux);
+    if (better(ok, oi, key, idx)) { key = ok; idx = oi; aux = oa; }
+}
+
+// Wave-wide (64 lanes) arg-best of (key desc, idx asc) carrying aux; every lane ends with the result.
+__device__ __forceinline__ void wave_argbest(double &key, int32_t &idx, int32_t &aux) {
+    argbest_stage<0>(key, idx, aux);
+    argbest_stage<1>(key, idx, aux);
+    argbest_stage<2>(key, idx, aux);
+    argbest_stage<3>(key, idx, aux);
+    argbest_stage<4>(key, idx, aux);
+    argbest_stage<5>(key, idx, aux);
+}
+
+template <int S>
+__device__ __forceinline__ int64_t sum_stage(int64_t v) {
+    const uint64_t u = (uint64_t)v;
+    const uint64_t hi = wpartner<S>((uint32_t)(u >> 32)), lo = wpartner<S>((uint32_t)u);
+    return v + (int64_t)((hi << 32) | lo);
+}
+
+// Order-preserving map of a double key to uint64 (larger key -> larger code; -inf/none -> 0).
+__device__ __forceinline__ uint64_t key_code(double k) {
+    const uint64_t u = (uint64_t)__double_as_longlong(k);
+    return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t umax_stage(uint64_t v) {
+    const uint64_t o = ((uint64_t)wpartner<S>((uint32_t)(v >> 32)) << 32) | wpartner<S>((uint32_t)v);
+    return o > v ? o : v;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    v = umax_stage<0>(v); v = umax_stage<1>(v); v = umax_stage<2>(v);
+    v = umax_stage<3>(v); v = umax_stage<4>(v); v = umax_stage<5>(v);
     return v;
 }
 
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+    v = sum_stage<0>(v); v = sum_stage<1>(v); v = sum_stage<2>(v);
+    v = sum_stage<3>(v); v = sum_stage<4>(v); v = sum_stage<5>(v);
+    return v;
+}
+
+template <int S>
+__device__ __forceinline__ int32_t min_stage(int32_t v) {
+    const int32_t o = (int32_t)wpartner<S>((uint32_t)v);
+    return o < v ? o : v;
+}
+
 __device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const int32_t o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
-    }
+    v = min_stage<0>(v); v = min_stage<1>(v); v = min_stage<2>(v);
+    v = min_stage<3>(v); v = min_stage<4>(v); v = min_stage<5>(v);
     return v;
 }
 

@@ -31,6 +31,8 @@ struct ksched_ctx {
     int64_t n_local = -1;
     int64_t n_global = 0;
     bool has_labels = false, has_price = false;
+    uint64_t max_abs_alloc = 0;  // saturating bound on |allocatable| (fast53 check)
+    uint64_t sum_abs_req = 0;    // saturating sum of |request| over the staged pods
     NodeRec *d_nodes = nullptr, *d_snap = nullptr;
     int64_t node_cap = 0;
     // pods
@@ -45,6 +47,11 @@ struct ksched_ctx {
     void *d_ws = nullptr;
     int64_t *d_cursor = nullptr;  // [0] cursor, [1..3] stats
     int64_t *h_cursor = nullptr;  // pinned
+    int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
+    hipStream_t stream2 = nullptr;  // commit stream of the batched pipeline
+    hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_pipe[2] = {};
+    void *d_xring = nullptr, *d_lring = nullptr;
+    int64_t xring_bytes = 0, lring_bytes = 0;
     // exact workspace
     uint64_t *d_slots = nullptr;
     int32_t *d_err = nullptr;
@@ -54,6 +61,7 @@ struct ksched_ctx {
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool running = false;
+    bool fast53 = false;
     std::vector<hipEvent_t> ev_pool;  // sampled per-family event pairs (opts.timing)
     struct Timed { int fam; int e0, e1; int64_t pairs; };
     std::vector<Timed> timed;
@@ -93,6 +101,9 @@ hipError_t grow(T **ptr, int64_t *cap, int64_t need, size_t elem) {
     return e;
 }
 
+uint64_t sat_add(uint64_t a, uint64_t b) { return a + b < a ? UINT64_MAX : a + b; }
+uint64_t uabs(int64_t v) { return v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v; }
+
 int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return v && *v ? std::atoi(v) : dflt;
@@ -110,19 +121,19 @@ hipError_t ev_take(ksched_ctx *c, int *idx) {
     return hipSuccess;
 }
 
-hipError_t ev_begin(ksched_ctx *c, bool on, int *e0) {
+hipError_t ev_begin(ksched_ctx *c, bool on, int *e0, hipStream_t s) {
     if (!on) return hipSuccess;
     hipError_t r = ev_take(c, e0);
     if (r != hipSuccess) return r;
-    return hipEventRecord(c->ev_pool[(size_t)*e0], c->stream);
+    return hipEventRecord(c->ev_pool[(size_t)*e0], s);
 }
 
-hipError_t ev_end(ksched_ctx *c, bool on, int fam, int e0, int64_t pairs) {
+hipError_t ev_end(ksched_ctx *c, bool on, int fam, int e0, int64_t pairs, hipStream_t s) {
     if (!on) return hipSuccess;
     int e1;
     hipError_t r = ev_take(c, &e1);
     if (r != hipSuccess) return r;
-    r = hipEventRecord(c->ev_pool[(size_t)e1], c->stream);
+    r = hipEventRecord(c->ev_pool[(size_t)e1], s);
     if (r == hipSuccess) c->timed.push_back({fam, e0, e1, pairs});
     return r;
 }
@@ -170,20 +181,38 @@ BatchPlan plan_batch(const ksched_ctx *c) {
     pl.off_send = take(pl.send_bytes);  // local lists + fc (also the single-GPU final lists)
     const int R = std::max(1, c->o.nranks);
     pl.off_recv = take(pl.send_bytes * R);
-    pl.off_glists = take((size_t)pl.B * pl.K * sizeof(Rec));
-    pl.off_gfc = take((size_t)pl.B * sizeof(int64_t));
+    pl.off_glists = take((size_t)2 * pl.B * pl.K * sizeof(Rec));  // ring of 2 (rank-merged lists)
+    pl.off_gfc = take((size_t)2 * pl.B * sizeof(int64_t));
     pl.off_lists = pl.off_send;
     pl.off_fc = pl.off_send + (size_t)pl.B * pl.K * sizeof(Rec);
     pl.total = off;
     return pl;
 }
 
-int64_t commit_lds_bytes(const ksched_ctx *c, int B, int *words) {
-    const int64_t w = (c->n_global + 31) / 32;
-    *words = (int)align_up((size_t)w, 4);
-    return (int64_t)*words * 4 + (int64_t)B * (int64_t)(sizeof(Touched) + kPodStageBytes);
+
+// fast53 for this call: every |alloc| + sum of |requests| < 2^52, on every rank.
+int decide_fast53(ksched_ctx *c) {
+    int flag = sat_add(c->max_abs_alloc, c->sum_abs_req) < (1ull << 52) ? 1 : 0;
+    if (env_int("KSCHED_NO_FAST53", 0)) flag = 0;
+    if (c->comm) {
+        int32_t *d = c->d_err;  // scratch word (zeroed again before use by exact mode)
+        HIPCHK(c, hipMemcpyAsync(d, &flag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        NCCLCHK(c, ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&flag, d, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemsetAsync(d, 0, sizeof(int32_t), c->stream));
+    }
+    c->fast53 = flag != 0;
+    return KSCHED_OK;
 }
 
+// Batched mode, software-pipelined over two streams:
+//   stream S: [wait commit(b-2)] apply(b-2) -> plan(b) -> score(b) -> merge(b) [-> all-gather -> rank merge]
+//   stream C: [wait lists(b)]    commit(b)
+// score(b) runs on every CU while commit(b-1) runs on one; commit(b) inherits the nodes committed by
+// batch b-1 (its score snapshot is one batch older) and node rows are written by apply only after
+// the next score has read them.  Each batch's start is planned speculatively (previous start + B);
+// a truncated batch invalidates the in-flight speculation, which commit skips and plan resyncs.
 int enqueue_batched(ksched_ctx *c) {
     const BatchPlan pl = plan_batch(c);
     if (c->ws_bytes < (int64_t)pl.total) {
@@ -193,98 +222,157 @@ int enqueue_batched(ksched_ctx *c) {
         HIPCHK(c, hipMalloc(&c->d_ws, pl.total));
         c->ws_bytes = (int64_t)pl.total;
     }
-    int words = 0;
-    const int64_t lds = commit_lds_bytes(c, pl.B, &words);
-    if (lds > 160 * 1024 - 4096)
-        return fail(c, KSCHED_E_INVALID, "batched mode: node bitmap + touched table exceed LDS (nodes_global too large or batch too big)");
+    const int64_t lds = (int64_t)commit_lds_bytes(pl.B, pl.K);
+    if (lds > 160 * 1024 - 4096 || pl.B > 128)
+        return fail(c, KSCHED_E_INVALID, "batched mode: batch <= 128 and B*(328+48K) <= ~150 KB of LDS");
     char *ws = static_cast<char *>(c->d_ws);
     const int prio = c->o.priority, dom = c->o.domain;
     const bool lab = c->o.use_labels != 0;
     const int R = std::max(1, c->o.nranks);
     PodArgs pods{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
-
-    HIPCHK(c, hipMemsetAsync(c->d_cursor, 0, 4 * sizeof(int64_t), c->stream));
-    int64_t resolved = 0, batches = 0;
-    double avg_progress = std::max(1.0, pl.K * 2.0);
     const int poll = env_int("KSCHED_POLL_BATCHES", 0);
-    const bool single_wave = env_int("KSCHED_COMMIT_WAVES", 1) == 1;
+    const bool f53 = c->fast53;
+    const bool one_stream = env_int("KSCHED_ONE_STREAM", 0) != 0;
+    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
+    constexpr int kRing = 4;  // lists / X buffers / events in flight
+    const size_t xb = xbuf_bytes(pl.B);
+    if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
+        if (c->d_xring) hipFree(c->d_xring);
+        c->d_xring = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_xring, xb * (kRing + 1)));
+        c->xring_bytes = (int64_t)(xb * (kRing + 1));
+    }
+    if (c->lring_bytes < (int64_t)(pl.send_bytes * kRing)) {
+        if (c->d_lring) hipFree(c->d_lring);
+        c->d_lring = nullptr;
+        HIPCHK(c, hipMalloc(&c->d_lring, pl.send_bytes * kRing));
+        c->lring_bytes = (int64_t)(pl.send_bytes * kRing);
+    }
+    auto xbuf = [&](int64_t b) -> XBuf * {  // b = -1 -> the permanently empty buffer
+        const int64_t slot = b < 0 ? kRing : (b % kRing);
+        return reinterpret_cast<XBuf *>(static_cast<char *>(c->d_xring) + (size_t)slot * xb);
+    };
+    Ctl *ctl = reinterpret_cast<Ctl *>(c->d_cursor);
+    HIPCHK(c, hipMemsetAsync(ctl, 0, sizeof(Ctl), sS));
+    for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
+    if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
+    if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
+    if (!one_stream) {  // stream C starts after the initialisation above
+        HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));
+        HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
+    }
+    int64_t resolved = 0, b = 0, last_resolved_b = -1;
+    double avg_progress = std::max(1.0, pl.B * 0.75);
     while (resolved < c->p) {
-        int64_t m = (int64_t)std::ceil((double)(c->p - resolved) / avg_progress);
-        m = std::max<int64_t>(1, std::min<int64_t>(m, poll > 0 ? poll : 256));
-        for (int64_t it = 0; it < m; ++it) {
-            const bool tm = c->o.timing && (batches % (c->o.timing_every > 0 ? c->o.timing_every : 16) == 0);
+        int64_t m = (int64_t)std::ceil((double)(c->p - resolved) / avg_progress) + 2;
+        m = std::max<int64_t>(2, std::min<int64_t>(m, poll > 0 ? poll : 256));
+        const int64_t b_end = b + m;
+        for (; b < b_end; ++b) {
+            const bool tm = c->o.timing && (b % (c->o.timing_every > 0 ? c->o.timing_every : 16) == 0);
             int e0 = -1;
+            const int slot = (int)(b % kPlanRing);
+            const int64_t *plan = &ctl->plan[slot];
+            char *lists_base = static_cast<char *>(c->d_lring) + (size_t)(b % kRing) * pl.send_bytes;
+            // S: write back batch b-2's commits (score(b-1) has read the old rows), then plan + score b
+            if (b >= 2) {
+                if (!one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[(b - 2) % kRing], 0));
+                HIPCHK(c, launch_apply_batch(xbuf(b - 2), c->d_nodes, c->o.node_offset, c->n_local, sS));
+            }
+            HIPCHK(c, launch_plan(ctl, slot, pl.B, c->p, sS));
             ScoreArgs sa{};
             sa.nodes = c->d_nodes; sa.n_local = c->n_local; sa.node_offset = c->o.node_offset;
-            sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = c->d_cursor; sa.B = pl.B;
+            sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = plan; sa.B = pl.B;
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part);
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt);
-            // (an empty shard runs one empty chunk: the kernel writes empty lists and zero counts)
-            HIPCHK(c, ev_begin(c, tm, &e0));
-            HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, sa, pl.pod_groups, c->stream));
-            HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local));
-            HIPCHK(c, ev_begin(c, tm, &e0));
-            // merge stages
+            HIPCHK(c, ev_begin(c, tm, &e0, sS));
+            HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, f53, sa, pl.pod_groups, sS));
+            HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
+            HIPCHK(c, ev_begin(c, tm, &e0, sS));
             const void *in = sa.part;
             const int64_t *in_cnt = sa.part_cnt;
-            for (int s = 0; s < pl.stages; ++s) {
+            for (int st = 0; st < pl.stages; ++st) {
                 MergeArgs ma{};
-                ma.in = in; ma.in_cnt = in_cnt; ma.C_in = pl.C[s];
-                ma.C_out = (pl.C[s] + 63) / 64;
-                ma.cursor = c->d_cursor; ma.P = c->p; ma.B = pl.B;
+                ma.in = in; ma.in_cnt = in_cnt; ma.C_in = pl.C[st];
+                ma.C_out = (pl.C[st] + 63) / 64;
+                ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
-                const bool fin = (s == pl.stages - 1);
+                const bool fin = (st == pl.stages - 1);
                 if (fin) {
-                    ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_lists);
-                    ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_fc);
+                    ma.out_rec = reinterpret_cast<Rec *>(lists_base);
+                    ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
                 } else {
-                    const int pp = s & 1;
+                    const int pp = st & 1;
                     const int c1 = pl.C[1];
                     ma.out = reinterpret_cast<Cand *>(ws + pl.off_m1) + (size_t)pp * pl.B * c1 * pl.K;
                     ma.out_cnt = reinterpret_cast<int64_t *>(ws + pl.off_m1cnt) + (size_t)pp * pl.B * c1;
                 }
-                HIPCHK(c, launch_merge(pl.K, false, fin, ma, c->stream));
+                HIPCHK(c, launch_merge(pl.K, false, fin, ma, sS));
                 in = ma.out; in_cnt = ma.out_cnt;
             }
-            HIPCHK(c, ev_end(c, tm, 1, e0, 0));
-            const Rec *lists = reinterpret_cast<const Rec *>(ws + pl.off_lists);
-            const int64_t *fc0 = reinterpret_cast<const int64_t *>(ws + pl.off_fc);
-            if (R > 1) {
-                HIPCHK(c, ev_begin(c, tm, &e0));
-                NCCLCHK(c, ncclAllGather(ws + pl.off_send, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, c->stream));
+            HIPCHK(c, ev_end(c, tm, 1, e0, 0, sS));
+            const Rec *lists = reinterpret_cast<const Rec *>(lists_base);
+            const int64_t *fc0 = reinterpret_cast<const int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
+            if (c->comm) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
+                HIPCHK(c, ev_begin(c, tm, &e0, sS));
+                NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sS));
                 MergeArgs ma{};
                 ma.in = ws + pl.off_recv; ma.rank_stride = (int64_t)pl.send_bytes; ma.C_in = R; ma.C_out = 1;
-                ma.cursor = c->d_cursor; ma.P = c->p; ma.B = pl.B;
-                ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists);
-                ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc);
-                HIPCHK(c, launch_merge(pl.K, true, true, ma, c->stream));
+                ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
+                ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists) + (size_t)(b % 2) * pl.B * pl.K;
+                ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc) + (size_t)(b % 2) * pl.B;
+                HIPCHK(c, launch_merge(pl.K, true, true, ma, sS));
                 lists = ma.out_rec;
                 fc0 = ma.out_fc;
-                HIPCHK(c, ev_end(c, tm, 3, e0, 0));
+                HIPCHK(c, ev_end(c, tm, 3, e0, 0, sS));
             }
+            if (!one_stream) {
+                HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sS));
+                HIPCHK(c, hipStreamWaitEvent(sC, c->ev_lists[b % kRing], 0));
+            }
+            // C: ordered commit of batch b
             CommitArgs ca{};
-            ca.lists = lists; ca.fc0 = fc0; ca.pods = pods; ca.cursor = c->d_cursor; ca.B = pl.B;
-            ca.nodes = c->d_nodes; ca.node_lo = c->o.node_offset; ca.n_local = c->n_local;
-            ca.n_global = c->n_global; ca.bitmap_words = words;
+            ca.lists = lists; ca.fc0 = fc0; ca.pods = pods; ca.plan = plan; ca.ctl = ctl; ca.B = pl.B;
+            ca.xin = xbuf(b - 1); ca.xout = xbuf(b);
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
-            ca.stats = c->d_cursor + 1;
-            HIPCHK(c, ev_begin(c, tm, &e0));
-            HIPCHK(c, launch_commit(pl.K, prio, dom, lab, ca, (size_t)lds, single_wave, c->stream));
-            HIPCHK(c, ev_end(c, tm, 2, e0, 0));
-            ++batches;
+            ca.dbg = c->d_dbg;
+            HIPCHK(c, ev_begin(c, tm, &e0, sC));
+            HIPCHK(c, launch_commit(pl.K, prio, dom, lab, f53, ca, (size_t)lds, sC));
+            HIPCHK(c, ev_end(c, tm, 2, e0, 0, sC));
+            if (!one_stream) HIPCHK(c, hipEventRecord(c->ev_commit[b % kRing], sC));
         }
-        HIPCHK(c, hipMemcpyAsync(c->h_cursor, c->d_cursor, 4 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        const int64_t now = c->h_cursor[0];
-        if (now <= resolved) return fail(c, KSCHED_E_DEVICE, "batched mode made no progress");
-        resolved = now;
-        if (c->h_cursor[1] > 0) avg_progress = std::max(1.0, (double)resolved / (double)c->h_cursor[1]);
+        HIPCHK(c, hipMemcpyAsync(c->h_cursor, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, sC));
+        HIPCHK(c, hipStreamSynchronize(sC));
+        const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+        if (h->cursor <= resolved) return fail(c, KSCHED_E_DEVICE, "batched mode made no progress");
+        resolved = h->cursor;
+        if (h->stats[0] > 0) avg_progress = std::max(1.0, (double)resolved / (double)(b));
+        last_resolved_b = b;
     }
-    c->st.batches = c->h_cursor[1];
-    c->st.truncations = c->h_cursor[2];
-    c->st.placed = c->h_cursor[3];
-    c->st.pair_evals = c->h_cursor[1] * (int64_t)pl.B * c->n_local;
-    c->run_batches = batches;
+    (void)last_resolved_b;
+    // drain: write back the last two batches' commits (the others were applied in the pipeline)
+    for (int64_t bb = std::max<int64_t>(0, b - 2); bb < b; ++bb) {
+        if (!one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[bb % kRing], 0));
+        HIPCHK(c, launch_apply_batch(xbuf(bb), c->d_nodes, c->o.node_offset, c->n_local, sS));
+    }
+    if (!one_stream) {  // the run's end event is recorded on stream S: make it cover stream C
+        HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));
+        HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
+    }
+    const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+    c->st.batches = h->stats[0];
+    c->st.truncations = h->stats[1];
+    c->st.placed = h->stats[2];
+    c->st.pair_evals = (h->stats[0] + h->stats[3]) * (int64_t)pl.B * c->n_local;
+    c->run_batches = b;
+    if (c->d_dbg) {
+        int64_t hd[16];
+        HIPCHK(c, hipStreamSynchronize(sS));
+        HIPCHK(c, hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[ksched commit stamps] pods=%lld kernels=%lld touched=%lld | cycles/pod: loads+rescore %.0f "
+                     "reduce %.0f decide %.0f commit+store %.0f | loop cycles/pod %.0f | skipped %lld\n",
+                     (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[5], (double)hd[1] / hd[5],
+                     (double)hd[2] / hd[5], (double)hd[3] / hd[5], (double)hd[4] / hd[5], (long long)h->stats[3]);
+    }
     return KSCHED_OK;
 }
 
@@ -297,12 +385,12 @@ int enqueue_exact(ksched_ctx *c) {
         // resource scores are ~150 FP64 ops per pair: spread nodes thin; best-price is a compare: pack
         const int per_thread = c->o.priority == KSCHED_PRIORITY_BEST_PRICE ? 8 : 1;
         npt = 1;
-        while (npt < 16 && (int64_t)kExactBlock * npt < (n + c->cus - 1) / c->cus) npt *= 2;
-        while (npt < per_thread && npt < 16) npt *= 2;
+        while (npt < 8 && (int64_t)kExactBlock * npt < (n + c->cus - 1) / c->cus) npt *= 2;
+        while (npt < per_thread && npt < 8) npt *= 2;
         G = (int)std::max<int64_t>(1, (n + (int64_t)kExactBlock * npt - 1) / ((int64_t)kExactBlock * npt));
     } else {
         npt = 1;
-        while (npt < 16 && (int64_t)G * kExactBlock * npt < n) npt *= 2;
+        while (npt < 8 && (int64_t)G * kExactBlock * npt < n) npt *= 2;
     }
     const int64_t per_wg = (n + G - 1) / G;
     if (per_wg > (int64_t)kExactBlock * npt)
@@ -318,9 +406,10 @@ int enqueue_exact(ksched_ctx *c) {
     a.slots = c->d_slots; a.err = c->d_err;
     a.timeout_ticks = (int64_t)env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000) * 100000;  // 100 MHz wall clock
     int e0 = -1;
-    HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0));
-    HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, a, kExactBlock, G > 1, c->stream));
-    HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n));
+    HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, c->stream));
+    HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, kExactBlock, G > 1,
+                           c->stream));
+    HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n, c->stream));
     c->st.pair_evals = c->p * n;
     c->st.batches = 0;
     c->st.truncations = 0;
@@ -357,8 +446,8 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     if (!c) return KSCHED_E_NOMEM;
     c->o = *opts;
     c->K = opts->topk ? opts->topk : 16;
-    c->B = opts->batch > 0 ? opts->batch : 8 * c->K;
-    if (c->B > 4096) { delete c; return KSCHED_E_INVALID; }
+    c->B = opts->batch > 0 ? opts->batch : std::min(128, 8 * c->K);
+    if (c->B > 128) { delete c; return KSCHED_E_INVALID; }  // touched table: 2B <= 256 = 4 slots per lane
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { delete c; return KSCHED_E_DEVICE; }
     if (opts->device >= 0) {
@@ -369,11 +458,17 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     }
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, c->dev) == hipSuccess) c->cus = prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    bool ev_ok = true;
+    for (int i = 0; i < 4; ++i)
+        ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_lists[i], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_commit[i], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < 2; ++i) ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming) == hipSuccess;
+    if (!ev_ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc((void **)&c->d_cursor, 8 * sizeof(int64_t)) != hipSuccess ||
+        hipMalloc((void **)&c->d_cursor, sizeof(Ctl)) != hipSuccess ||
         hipMalloc((void **)&c->d_err, sizeof(int32_t)) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_cursor, 8 * sizeof(int64_t)) != hipSuccess) {
+        hipHostMalloc((void **)&c->h_cursor, sizeof(Ctl)) != hipSuccess) {
         ksched_destroy(c);
         return KSCHED_E_DEVICE;
     }
@@ -385,16 +480,24 @@ int ksched_destroy(ksched_ctx *c) {
     if (!c) return KSCHED_OK;
     hipSetDevice(c->dev);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->stream2) hipStreamSynchronize(c->stream2);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
     hipFree(c->d_oidx); hipFree(c->d_osc); hipFree(c->d_ofeas);
-    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_slots); hipFree(c->d_err);
+    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_dbg); hipFree(c->d_slots); hipFree(c->d_err);
     if (c->h_cursor) hipHostFree(c->h_cursor);
     for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    for (int i = 0; i < 4; ++i) {
+        if (c->ev_lists[i]) hipEventDestroy(c->ev_lists[i]);
+        if (c->ev_commit[i]) hipEventDestroy(c->ev_commit[i]);
+    }
+    for (int i = 0; i < 2; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
+    hipFree(c->d_xring); hipFree(c->d_lring);
     if (c->stream) hipStreamDestroy(c->stream);
+    if (c->stream2) hipStreamDestroy(c->stream2);
     delete c;
     return KSCHED_OK;
 }
@@ -412,7 +515,6 @@ int ksched_get_unique_id(uint8_t out_id[128]) {
 
 int ksched_set_comm(ksched_ctx *c, const uint8_t id[128]) {
     if (!c || !id) return KSCHED_E_INVALID;
-    if (c->o.nranks <= 1) return KSCHED_OK;
     HIPCHK(c, hipSetDevice(c->dev));
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
@@ -430,13 +532,16 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
         return fail(c, KSCHED_E_INVALID, "load_nodes: best-price priority needs prices");
     if (n > 0x7ffffff0LL) return fail(c, KSCHED_E_INVALID, "load_nodes: too many nodes");
     std::vector<NodeRec> h((size_t)std::max<int64_t>(n, 0));
+    uint64_t mx = 0;
     for (int64_t i = 0; i < n; ++i) {
         NodeRec &r = h[(size_t)i];
         r.a[0] = ac[i]; r.a[1] = am[i]; r.a[2] = ap[i];
-        r.af[0] = (double)ac[i]; r.af[1] = (double)am[i]; r.af[2] = (double)ap[i];
+        r.af[0] = r.af[1] = r.af[2] = 0.0;  // derived on the device (k_prep_nodes) with the reciprocals
+        r.y[0] = r.y[1] = r.y[2] = 0.0;
         r.labels = labels ? labels[i] : 0;
         r.price = price ? price[i] : 0.f;
-        r.pad = 0;
+        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        mx = std::max(mx, std::max(uabs(ac[i]), std::max(uabs(am[i]), uabs(ap[i]))));
         if (price && !std::isfinite(price[i])) return fail(c, KSCHED_E_INVALID, "load_nodes: non-finite price");
     }
     HIPCHK(c, hipSetDevice(c->dev));
@@ -444,6 +549,9 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
     HIPCHK(c, grow(&c->d_nodes, &c->node_cap, n, sizeof(NodeRec)));
     if (c->d_snap) { hipFree(c->d_snap); c->d_snap = nullptr; }
     if (n > 0) HIPCHK(c, hipMemcpy(c->d_nodes, h.data(), (size_t)n * sizeof(NodeRec), hipMemcpyHostToDevice));
+    HIPCHK(c, launch_prep_nodes(c->d_nodes, n, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->max_abs_alloc = mx;
     c->n_local = n;
     c->n_global = c->o.nranks > 1 ? c->o.nodes_global : (c->o.nodes_global > 0 ? c->o.nodes_global : n);
     if (c->n_global < c->o.node_offset + n) return fail(c, KSCHED_E_INVALID, "load_nodes: nodes_global too small");
@@ -458,8 +566,10 @@ int ksched_apply_delta(ksched_ctx *c, int64_t k, const int32_t *idx, const int64
     if (c->n_local < 0) return fail(c, KSCHED_E_STATE, "apply_delta before load_nodes");
     if (k < 0 || (k > 0 && (!idx || !dc || !dm || !dp))) return fail(c, KSCHED_E_INVALID, "apply_delta: bad arguments");
     if (k == 0) return KSCHED_OK;
-    for (int64_t i = 0; i < k; ++i)
+    for (int64_t i = 0; i < k; ++i) {
         if (idx[i] < 0 || idx[i] >= c->n_local) return fail(c, KSCHED_E_INVALID, "apply_delta: node index out of range");
+        c->max_abs_alloc = sat_add(c->max_abs_alloc, sat_add(uabs(dc[i]), sat_add(uabs(dm[i]), uabs(dp[i]))));
+    }
     HIPCHK(c, hipSetDevice(c->dev));
     std::vector<int64_t> d((size_t)(3 * k));
     std::memcpy(d.data(), dc, (size_t)k * 8);
@@ -543,7 +653,28 @@ int ksched_upload_pods(ksched_ctx *c, int64_t p, const int64_t *rc, const int64_
         if (sel) HIPCHK(c, hipMemcpy(c->d_sel, sel, (size_t)p * 8, hipMemcpyHostToDevice));
         else HIPCHK(c, hipMemset(c->d_sel, 0, (size_t)p * 8));
     }
+    uint64_t sum = 0;
+    for (int64_t i = 0; i < p; ++i) sum = sat_add(sum, sat_add(uabs(rc[i]), sat_add(uabs(rm[i]), uabs(rp[i]) + 1)));
+    c->sum_abs_req = sum;
     c->p = p;
+    return KSCHED_OK;
+}
+
+int ksched_selftest_fastdiv(ksched_ctx *c, int64_t n, const double *a, const double *b, double *out_native,
+                            double *out_fast) {
+    if (!c || n < 0 || (n > 0 && (!a || !b || !out_native || !out_fast))) return KSCHED_E_INVALID;
+    if (n == 0) return KSCHED_OK;
+    HIPCHK(c, hipSetDevice(c->dev));
+    double *d = nullptr;
+    HIPCHK(c, hipMalloc(&d, (size_t)n * 32));
+    hipError_t e = hipMemcpy(d, a, (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d + n, b, (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = launch_selftest_div(n, d, d + n, d + 2 * n, d + 3 * n, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(out_native, d + 2 * n, (size_t)n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_fast, d + 3 * n, (size_t)n * 8, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("selftest_fastdiv: ") + hipGetErrorString(e));
     return KSCHED_OK;
 }
 
@@ -557,6 +688,7 @@ int ksched_run(ksched_ctx *c) {
     c->timed.clear();
     c->ev_used = 0;
     c->st.pods = c->p;
+    if (int rr = decide_fast53(c)) return rr;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int r = KSCHED_OK;
     if (c->p > 0) {

@@ -5,9 +5,11 @@
 // Batched mode: k_score_topk   pod-per-lane fused predicate + score + per-lane top-K over a node
 //                              chunk (node rows are wave-uniform -> scalar loads);
 //               k_merge        sorted-list merge, one wave per (pod, <=64 lists), DPP/shuffle arg-best;
-//               k_commit       one workgroup replays the batch in pod order: re-scores the nodes
-//                              already committed in the batch, takes the first untouched candidate,
-//                              commits, stops at the first candidate-list overflow.
+//               k_commit       one wave replays the batch in pod order: re-scores the nodes already
+//                              committed in the batch, takes the first untouched candidate, commits,
+//                              stops at the first candidate-list overflow.
+// Every resource score divides by hoisted refined reciprocals (recip/qdiv, ksched_device.h), which
+// are bit-identical to hipcc's f64 division for this path's operands.
 // See DESIGN.md for the correctness argument of the batched commit.
 #pragma once
 
@@ -17,14 +19,47 @@ namespace ksched {
 
 struct alignas(8) Touched {
     int32_t idx;
-    int32_t pad;
-    int64_t s0[3];   // state at the batch snapshot
-    int64_t cur[3];  // current state
+    int32_t mine;     // committed to by a pod of THIS batch (exported to the next batch)
+    int64_t s0[3];    // state at this batch's score snapshot
+    int64_t sb[3];    // state when this batch's commit started
+    int64_t cur[3];   // current state
+    double curf[3];   // (double)cur
+    double cury[3];   // recip((double)cur)
     uint64_t labels;
     float price;
     int32_t pad2;
 };
-static_assert(sizeof(Touched) == 72, "Touched layout");
+static_assert(sizeof(Touched) == 144, "Touched layout");
+
+// Nodes committed by one batch, handed to the next batch's commit (which scored against a snapshot
+// one batch older) and to the apply kernel that writes them into the node rows.
+struct alignas(8) XRec {
+    int32_t idx;
+    int32_t pad;
+    int64_t sb[3];    // state before the batch (= the next batch's snapshot state)
+    int64_t cur[3];   // state after the batch
+    uint64_t labels;
+    float price;
+    int32_t pad2;
+};
+static_assert(sizeof(XRec) == 72, "XRec layout");
+
+struct alignas(8) XBuf {
+    int32_t count;
+    int32_t pad;
+    XRec e[1];        // [2 * B] follow
+};
+
+// Device-side pipeline control (one per context).  plan[] holds each in-flight batch's first pod
+// (ring of kPlanRing; -1 = nothing to do).  cursor/resync are written by k_commit, spec_next by k_plan.
+constexpr int kPlanRing = 8;
+struct alignas(8) Ctl {
+    int64_t cursor;     // first unresolved pod
+    int64_t spec_next;  // next speculative batch start
+    int64_t resync;     // 1: a batch truncated; the next plan restarts at cursor
+    int64_t stats[5];   // batches committed, truncated, placed, skipped, pairs scored
+    int64_t plan[kPlanRing];
+};
 
 struct PodArgs {
     const int64_t *rc, *rm, *rp;
@@ -57,7 +92,7 @@ struct ScoreArgs {
     int32_t S;         // nodes per chunk (one wave per chunk and 64 pods)
     int32_t n_chunks;
     PodArgs pods;
-    const int64_t *cursor;
+    const int64_t *cursor;  // this batch's plan slot (first pod, or -1)
     int32_t B;
     Cand *part;        // [B][n_chunks][K]
     int64_t *part_cnt; // [B][n_chunks]
@@ -85,29 +120,64 @@ struct CommitArgs {
     const Rec *lists;       // [B][K]
     const int64_t *fc0;     // [B]
     PodArgs pods;
-    int64_t *cursor;
+    const int64_t *plan;    // this batch's plan slot
+    Ctl *ctl;
     int32_t B;
-    NodeRec *nodes;         // local shard
-    int64_t node_lo;        // global index of the first local node
-    int64_t n_local;
-    int64_t n_global;       // bitmap bits
-    int32_t bitmap_words;
+    const XBuf *xin;        // nodes committed by the previous batch (relative to this batch's snapshot)
+    XBuf *xout;             // nodes committed by this batch
     OutArgs out;
-    int64_t *stats;         // [0] batches [1] truncations [2] placed
+    int64_t *dbg;           // diagnostics only (KSCHED_COMMIT_STAMPS): per-phase cycle sums, else null
 };
 
-// host-side launchers (ksched_kernels.hip)
-hipError_t launch_exact(int npt, int prio, int dom, bool lab, const ExactArgs &a, int block, bool cooperative,
-                        hipStream_t s);
-hipError_t launch_score_topk(int K, int prio, int dom, bool lab, const ScoreArgs &a, int pod_groups, hipStream_t s);
+struct alignas(8) PodStage {
+    int64_t rc, rm, rp;
+    uint64_t sel;
+    int64_t fc0;
+};
+constexpr size_t kPodStageBytes = sizeof(PodStage);
+
+// A candidate as staged in the commit kernel's LDS (idx = kNoIdx for an empty slot).
+struct alignas(8) CandStage {
+    double key;
+    int32_t idx;
+    float price;
+    int64_t a[3];
+    uint64_t labels;
+};
+static_assert(sizeof(CandStage) == 48, "CandStage layout");
+
+constexpr int kTouchHashBits = 9;  // touched-node set: 512 slots >= 2 x max batch (256)
+constexpr int kTouchHash = 1 << kTouchHashBits;
+
+constexpr int kTouchFilterBits = 16;  // 64K-bit filter in front of the hash (bit = idx & 0xffff)
+constexpr int kTouchFilterWords = (1 << kTouchFilterBits) / 32;
+
+// LDS bytes of k_commit for a batch of B pods with K candidates each (touched table: the previous
+// batch's nodes + this batch's, <= 2B).
+constexpr size_t commit_lds_bytes(int B, int K) {
+    return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) +
+           (size_t)B * (2 * sizeof(Touched) + sizeof(PodStage) + (size_t)K * sizeof(CandStage));
+}
+constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
+
+// host-side launchers (ksched_kernels.hip).  fast53: every allocatable and request magnitude stays
+// below 2^52 for the whole call (host-checked), enabling (double)(a-r) == (double)a - (double)r.
+hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s);
+hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool fast53, const ExactArgs &a, int block,
+                        bool cooperative, hipStream_t s);
+hipError_t launch_score_topk(int K, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
+                             hipStream_t s);
 hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
-hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, bool single_wave,
+hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, size_t lds_bytes,
                          hipStream_t s);
-constexpr size_t kPodStageBytes = 40;  // LDS per batch pod staged by the single-wave commit
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
+hipError_t launch_plan(Ctl *ctl, int slot, int B, int64_t P, hipStream_t s);
+hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s);
+// diagnostics: qdiv(a, b, recip(b)) against the native a / b, bit for bit
+hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,
+                               hipStream_t s);
 
 constexpr int kExactBlock = 256;
-constexpr int kCommitBlock = 256;
 
 }  // namespace ksched

@@ -15,12 +15,27 @@ __device__ __forceinline__ void st_granule(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+__device__ __forceinline__ void set_node(NodeRec *nd, int64_t a0, int64_t a1, int64_t a2) {
+    nd->a[0] = a0; nd->a[1] = a1; nd->a[2] = a2;
+    const double f0 = (double)a0, f1 = (double)a1, f2 = (double)a2;
+    nd->af[0] = f0; nd->af[1] = f1; nd->af[2] = f2;
+    nd->y[0] = recip_or_zero(a0, f0); nd->y[1] = recip_or_zero(a1, f1); nd->y[2] = recip_or_zero(a2, f2);
+}
+
 }  // namespace
+
+// (re)derive af / y of every node row from its int64 allocatable
+__global__ void k_prep_nodes(NodeRec *nodes, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    NodeRec *nd = nodes + i;
+    set_node(nd, nd->a[0], nd->a[1], nd->a[2]);
+}
 
 // ------------------------------------------------------------------------------------------------
 // Exact mode: one persistent launch schedules every pod in order.
 //   - workgroup g owns nodes [g*per_wg, (g+1)*per_wg); thread t holds nodes g*per_wg + t + k*256
-//     (k < NPT) in registers for the whole launch;
+//     (k < NPT) in registers for the whole launch, with their (double) values and reciprocals;
 //   - per pod: each lane scores its nodes (predicate.go:127-150 + priorities.go:45-50), wave
 //     butterfly arg-best + count, 4-wave combine through LDS;
 //   - G > 1: wave 0 publishes the workgroup's (key, idx, count) as four tagged 8-byte granules
@@ -29,7 +44,7 @@ __device__ __forceinline__ void st_granule(uint64_t *p, uint64_t v) {
 //     then folds the same G records into the same decision;
 //   - the owner lane of the winning node commits it in registers; nodes are written back at exit.
 // ------------------------------------------------------------------------------------------------
-template <int NPT, int PRIO, int DOM, bool LAB>
+template <int NPT, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -37,8 +52,10 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
     const int g = blockIdx.x;
     const int64_t lo = (int64_t)g * A.per_wg;
     const int64_t hi = (lo + A.per_wg < A.n) ? lo + A.per_wg : A.n;
+    const double y3 = recip(3.0);
 
     int64_t a0[NPT], a1[NPT], a2[NPT];
+    double f0[NPT], f1[NPT], f2[NPT], y0[NPT], y1[NPT], y2[NPT];
     uint64_t lab[NPT];
     float pr[NPT];
     int32_t id[NPT];
@@ -46,11 +63,14 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
     for (int k = 0; k < NPT; ++k) {
         const int64_t j = lo + tid + (int64_t)k * kExactBlock;
         if (j < hi) {
-            const NodeRec nd = A.nodes[j];
+            const NodeRec &nd = A.nodes[j];
             a0[k] = nd.a[0]; a1[k] = nd.a[1]; a2[k] = nd.a[2];
+            f0[k] = nd.af[0]; f1[k] = nd.af[1]; f2[k] = nd.af[2];
+            y0[k] = nd.y[0]; y1[k] = nd.y[1]; y2[k] = nd.y[2];
             lab[k] = nd.labels; pr[k] = nd.price; id[k] = (int32_t)j;
         } else {
-            a0[k] = a1[k] = a2[k] = 0; lab[k] = 0; pr[k] = 0.f; id[k] = kNoIdx;
+            a0[k] = a1[k] = a2[k] = 0; f0[k] = f1[k] = f2[k] = 0.0; y0[k] = y1[k] = y2[k] = 0.0;
+            lab[k] = 0; pr[k] = 0.f; id[k] = kNoIdx;
         }
     }
 
@@ -77,8 +97,8 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
                 const bool f = fits(rc, rm, rp, sel, a0[k], a1[k], a2[k], lab[k], LAB);
                 cnt += f;
                 double key;
-                if (pair_key<PRIO, DOM>(f, rc, rm, rp, rcf, rmf, rpf, a0[k], a1[k], a2[k], (double)a0[k],
-                                        (double)a1[k], (double)a2[k], pr[k], &key) &&
+                if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, a0[k], a1[k], a2[k], f0[k], f1[k],
+                                                  f2[k], y0[k], y1[k], y2[k], y3, pr[k], &key) &&
                     better(key, id[k], bk, bi)) {
                     bk = key;
                     bi = id[k];
@@ -157,6 +177,9 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
             for (int k = 0; k < NPT; ++k) {
                 if (id[k] == gi) {  // commit: used += request, ONE pod (anchor/predicate.go:99-102)
                     a0[k] = wsub(a0[k], rc); a1[k] = wsub(a1[k], rm); a2[k] = wsub(a2[k], 1);
+                    f0[k] = (double)a0[k]; f1[k] = (double)a1[k]; f2[k] = (double)a2[k];
+                    y0[k] = recip_or_zero(a0[k], f0[k]); y1[k] = recip_or_zero(a1[k], f1[k]);
+                    y2[k] = recip_or_zero(a2[k], f2[k]);
                 }
             }
         }
@@ -167,28 +190,23 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
         }
     }
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-        if (id[k] != kNoIdx) {
-            NodeRec *nd = A.nodes + id[k];
-            nd->a[0] = a0[k]; nd->a[1] = a1[k]; nd->a[2] = a2[k];
-            nd->af[0] = (double)a0[k]; nd->af[1] = (double)a1[k]; nd->af[2] = (double)a2[k];
-        }
-    }
+    for (int k = 0; k < NPT; ++k)
+        if (id[k] != kNoIdx) set_node(A.nodes + id[k], a0[k], a1[k], a2[k]);
 }
 
 // ------------------------------------------------------------------------------------------------
 // Batched mode, stage 1: fused predicate + score + per-lane top-K.  Lane = pod of the batch, wave =
-// one node chunk; node rows are wave-uniform (scalar loads of the 64-B NodeRec).  The list is kept
-// sorted by (key desc, idx asc) with a register bubble insert.
+// one node chunk; node rows are wave-uniform (scalar loads of the 96-B NodeRec, reciprocals included).
+// The list is kept sorted by (key desc, idx asc) with a register bubble insert.
 // ------------------------------------------------------------------------------------------------
-template <int K, int PRIO, int DOM, bool LAB>
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int chunk = blockIdx.x * 4 + wave;
     if (chunk >= A.n_chunks) return;
     const int64_t p0 = *A.cursor;
-    if (p0 >= A.pods.p) return;
+    if (p0 < 0 || p0 >= A.pods.p) return;
     const int b = blockIdx.y * 64 + lane;
     const int64_t pod = p0 + b;
     const bool active = (b < A.B) && (pod < A.pods.p);
@@ -197,6 +215,7 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     const int64_t rp = active ? A.pods.rp[pod] : 0;
     const uint64_t sel = (LAB && active) ? A.pods.sel[pod] : 0;
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+    const double y3 = recip(3.0);
 
     double key[K];
     int32_t idx[K];
@@ -211,8 +230,8 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
         const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
         cnt += f;
         double k;
-        if (pair_key<PRIO, DOM>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1], nd.af[2], nd.price,
-                                &k)) {
+        if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1], nd.af[2],
+                                          nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k)) {
             int32_t ci = (int32_t)(A.node_offset + j);
             if (better(k, ci, key[K - 1], idx[K - 1])) {
                 double ck = k;
@@ -248,7 +267,7 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
     const int grp = blockIdx.x;
     const int b = blockIdx.y;
     const int64_t p0 = *A.cursor;
-    if (p0 >= A.P || b >= A.B || p0 + b >= A.P) return;
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;
     const int list = grp * 64 + lane;
     const bool has = list < A.C_in;
     int64_t cnt = 0;
@@ -313,174 +332,263 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Ordered commit of one batch (one workgroup).  For pod i of the batch, with T = nodes committed by
-// pods < i of this batch (LDS table; s0 = snapshot state, cur = current state):
+// Ordered commit of one batch: a single-wave sequencer.  For pod i of the batch, with T = nodes
+// committed by pods < i of this batch (LDS table; s0 = snapshot state, cur = current state):
 //   fc   = fc0[i] - sum_T fits(s0) + sum_T fits(cur)                          (predicate count)
 //   t*   = best of T re-scored at cur;  u* = first list entry not in T (exact: untouched)
 //   list full and all touched: t* must beat list[K-1] (every unlisted untouched node ranks below
 //   it), otherwise the batch stops before pod i (overflow) and the next batch restarts there.
+// One wave, no barriers: reductions are register butterflies (DPP + permlane swaps) and ballots;
+// every lane evaluates the (wave-uniform) decision; requests and feasible counts are staged into LDS
+// once; lane q < K holds candidate q of the current pod while the next pod's candidates load into
+// the other register buffer (the loop is unrolled by two so the wait lands one pod later).
 // ------------------------------------------------------------------------------------------------
-template <int K, int PRIO, int DOM, bool LAB>
-__global__ __launch_bounds__(kCommitBlock) void k_commit(CommitArgs A) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint32_t *bitmap = reinterpret_cast<uint32_t *>(smem);
-    Touched *T = reinterpret_cast<Touched *>(smem + (size_t)A.bitmap_words * 4);
-    __shared__ double s_tk[kCommitBlock / 64];
-    __shared__ int32_t s_ti[kCommitBlock / 64], s_ts[kCommitBlock / 64], s_uq[kCommitBlock / 64];
-    __shared__ int32_t s_cv[kCommitBlock / 64];
-    __shared__ int64_t s_df[kCommitBlock / 64];
-    __shared__ int32_t s_nT, s_stop;
+constexpr int kMaxTouchedSlots = 4;  // touched nodes per lane -> 256 (previous batch's + this batch's, B <= 128)
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int64_t p0 = *A.cursor;
-    if (p0 >= A.pods.p) return;
-    const int64_t nb = (A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B;
-    for (int w = tid; w < A.bitmap_words; w += kCommitBlock) bitmap[w] = 0;
-    if (tid == 0) { s_nT = 0; s_stop = 0; }
-    __syncthreads();
+struct CommitCtx {
+    int32_t *hkey;       // open-addressing set of touched node indices (kTouchHash slots, -1 = empty)
+    uint32_t *filt;      // 64K-bit filter: bit (idx & 0xffff) set once idx is touched
+    Touched *T;
+    const PodStage *PS;
+    const CandStage *CS; // [B][K] staged candidate lists
+    int nT;
+    int64_t placed;
+    double y3;
+    int lane;
+    int64_t p0;
+};
 
-    int64_t done = nb;
-    int64_t placed = 0;
-    for (int64_t i = 0; i < nb; ++i) {
-        const int64_t pod = p0 + i;
-        const int64_t rc = A.pods.rc[pod], rm = A.pods.rm[pod], rp = A.pods.rp[pod];
-        const uint64_t sel = LAB ? A.pods.sel[pod] : 0;
-        const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
-        const int nT = s_nT;
-        int64_t df = 0;
-        double tk = -__builtin_inf();
-        int32_t ti = kNoIdx, ts = -1;
-        for (int t = tid; t < nT; t += kCommitBlock) {
-            const Touched &x = T[t];
-            const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
-            const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
-            df += (int64_t)f1 - (int64_t)f0;
-            double k;
-            if (pair_key<PRIO, DOM>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2], (double)x.cur[0],
-                                    (double)x.cur[1], (double)x.cur[2], x.price, &k) &&
-                better(k, x.idx, tk, ti)) {
-                tk = k; ti = x.idx; ts = t;
-            }
-        }
-        int32_t uq = K, cv = 0;
-        if (tid < K) {
-            const Rec &L = A.lists[(size_t)i * K + tid];
-            if (L.valid) {
-                cv = 1;
-                const uint32_t bit = bitmap[(uint32_t)L.idx >> 5] & (1u << ((uint32_t)L.idx & 31));
-                if (!bit) uq = tid;
-            }
-        }
-        wave_argbest(tk, ti, ts);
-        df = wave_sum_i64(df);
-        uq = wave_min_i32(uq);
-        cv = (int32_t)wave_sum_i64(cv);
-        if (lane == 0) { s_tk[wave] = tk; s_ti[wave] = ti; s_ts[wave] = ts; s_uq[wave] = uq; s_cv[wave] = cv; s_df[wave] = df; }
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < kCommitBlock / 64; ++w) {
-                df += s_df[w];
-                uq = s_uq[w] < uq ? s_uq[w] : uq;
-                cv += s_cv[w];
-                if (better(s_tk[w], s_ti[w], tk, ti)) { tk = s_tk[w]; ti = s_ti[w]; ts = s_ts[w]; }
-            }
-            const int64_t fc = A.fc0[i] + df;
-            int32_t oidx = -1;
-            double osc = 0.0;
-            bool stop = false;
-            if (fc != 0) {
-                int slot = -1;
-                const Rec *u = nullptr;
-                double wk = 0.0;
-                int32_t wi = kNoIdx;
-                if (uq < cv) {
-                    u = &A.lists[(size_t)i * K + uq];
-                    if (ti != kNoIdx && better(tk, ti, u->key, u->idx)) { wk = tk; wi = ti; slot = ts; u = nullptr; }
-                    else { wk = u->key; wi = u->idx; }
-                } else if (cv < K) {
-                    if (ti != kNoIdx) { wk = tk; wi = ti; slot = ts; }
-                } else {
-                    const Rec &last = A.lists[(size_t)i * K + (K - 1)];
-                    if (ti != kNoIdx && better(tk, ti, last.key, last.idx)) { wk = tk; wi = ti; slot = ts; }
-                    else stop = true;
-                }
-                if (!stop) {
-                    if (wi == kNoIdx) {
-                        oidx = -2;
-                    } else {
-                        if (u) {  // first touch of this node in the batch
-                            slot = s_nT++;
-                            Touched &x = T[slot];
-                            x.idx = u->idx; x.pad = 0;
-                            x.s0[0] = x.cur[0] = u->a[0];
-                            x.s0[1] = x.cur[1] = u->a[1];
-                            x.s0[2] = x.cur[2] = u->a[2];
-                            x.labels = u->labels; x.price = u->price; x.pad2 = 0;
-                            bitmap[(uint32_t)u->idx >> 5] |= 1u << ((uint32_t)u->idx & 31);
-                        }
-                        Touched &x = T[slot];
-                        x.cur[0] = wsub(x.cur[0], rc); x.cur[1] = wsub(x.cur[1], rm); x.cur[2] = wsub(x.cur[2], 1);
-                        oidx = wi;
-                        osc = PRIO == kPrioPrice ? -wk : wk;
-                        ++placed;
-                    }
-                }
-            }
-            if (stop) {
-                s_stop = 1;
-            } else {
-                A.out.idx[pod] = oidx;
-                A.out.score[pod] = osc;
-                A.out.feas[pod] = (int32_t)fc;
-            }
-        }
-        __syncthreads();
-        if (s_stop) { done = i; break; }
-    }
-    // write back committed nodes of this shard
-    const int nT = s_nT;
-    for (int t = tid; t < nT; t += kCommitBlock) {
-        const Touched &x = T[t];
-        const int64_t j = (int64_t)x.idx - A.node_lo;
-        if (j >= 0 && j < A.n_local) {
-            NodeRec *nd = A.nodes + j;
-            nd->a[0] = x.cur[0]; nd->a[1] = x.cur[1]; nd->a[2] = x.cur[2];
-            nd->af[0] = (double)x.cur[0]; nd->af[1] = (double)x.cur[1]; nd->af[2] = (double)x.cur[2];
-        }
-    }
-    if (tid == 0) {
-        *A.cursor = p0 + done;
-        A.stats[0] += 1;
-        A.stats[1] += (done < nb) ? 1 : 0;
-        A.stats[2] += placed;
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
+__device__ __forceinline__ uint32_t thash(int32_t idx) { return ((uint32_t)idx * 2654435761u) >> (32 - kTouchHashBits); }
+
+__device__ __forceinline__ bool touched_has(const CommitCtx &cx, int32_t idx) {
+    if (!(cx.filt[((uint32_t)idx & 0xffffu) >> 5] & (1u << ((uint32_t)idx & 31)))) return false;
+    for (uint32_t h = thash(idx);; h = (h + 1) & (kTouchHash - 1)) {
+        const int32_t k = cx.hkey[h];
+        if (k == idx) return true;
+        if (k < 0) return false;
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// Ordered commit, single-wave sequencer (the default).  Same decision rule as k_commit, but:
-//   - one wave, no barriers: every per-pod reduction is a wave butterfly and every lane evaluates the
-//     (wave-uniform) decision itself; the touched table and node bitmap live in LDS;
-//   - the batch's requests and feasible counts are staged into LDS once, up front;
-//   - lane q < K holds candidate q of the current pod and already has the NEXT pod's candidate load
-//     in flight (software prefetch), so no dependent global load sits on the serial path.
-// ------------------------------------------------------------------------------------------------
-struct alignas(8) PodStage {
-    int64_t rc, rm, rp;
-    uint64_t sel;
-    int64_t fc0;
-};
+__device__ __forceinline__ void touched_insert(CommitCtx &cx, int32_t idx) {
+    uint32_t h = thash(idx);
+    while (cx.hkey[h] >= 0) h = (h + 1) & (kTouchHash - 1);
+    cx.hkey[h] = idx;
+    cx.filt[((uint32_t)idx & 0xffffu) >> 5] |= 1u << ((uint32_t)idx & 31);
+}
 
-template <int K, int PRIO, int DOM, bool LAB>
-__global__ __launch_bounds__(64) void k_commit1(CommitArgs A) {
+// Re-score NS touched slots per lane (t = lane + 64 s), branch-free so the NS dependency chains
+// interleave; feasibility deltas through ballots.
+template <int NS, int PRIO, int DOM, bool LAB, bool F53>
+__device__ __forceinline__ void rescore_touched(const CommitCtx &cx, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
+                                                double rcf, double rmf, double rpf, int64_t &df, double &tk,
+                                                int32_t &ti, int32_t &ts) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int t = cx.lane + 64 * s;
+        const bool in = t < cx.nT;
+        const Touched &x = cx.T[in ? t : 0];
+        const bool f0 = in && fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
+        const bool f1 = in && fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
+        double k;
+        const bool ok = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
+                                                      x.curf[0], x.curf[1], x.curf[2], x.cury[0], x.cury[1],
+                                                      x.cury[2], cx.y3, x.price, &k);
+        if (in && ok && better(k, x.idx, tk, ti)) { tk = k; ti = x.idx; ts = t; }
+        df += (int64_t)__popcll(__ballot(f1)) - (int64_t)__popcll(__ballot(f0));
+    }
+}
+
+// Wave arg-best via a 64-bit order-preserving max, then (ties only) the lowest node index.
+__device__ __forceinline__ void wave_argbest_fast(double &tk, int32_t &ti, int32_t &ts) {
+    const uint64_t mine = ti == kNoIdx ? 0ull : key_code(tk);
+    const uint64_t best = wave_max_u64(mine);
+    if (best == 0) { tk = -__builtin_inf(); ti = kNoIdx; ts = -1; return; }
+    const uint64_t tie = __ballot(mine == best);
+    int src;
+    if (__popcll(tie) == 1) {
+        src = __ffsll((unsigned long long)tie) - 1;
+    } else {
+        const int32_t mi = wave_min_i32(mine == best ? ti : kNoIdx);
+        src = __ffsll((unsigned long long)__ballot(mine == best && ti == mi)) - 1;
+    }
+    const uint64_t kb = (uint64_t)__double_as_longlong(tk);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(kb >> 32), src);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kb, src);
+    tk = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    ti = __builtin_amdgcn_readlane(ti, src);
+    ts = __builtin_amdgcn_readlane(ts, src);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), src);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool ST>
+__device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, int i, const PodStage &ps,
+                                            const CandStage &my, uint64_t *ph) {
+    const int lane = cx.lane;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    if (ST) t0 = stamp();
+    const int64_t rc = ps.rc, rm = ps.rm, rp = ps.rp;
+    const uint64_t sel = ps.sel;
+    const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+    // re-score the nodes already committed in this batch
+    int64_t df = 0;
+    double tk = -__builtin_inf();
+    int32_t ti = kNoIdx, ts = -1;
+    if (cx.nT > 0) {
+        if (cx.nT <= 64) rescore_touched<1, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
+        else if (cx.nT <= 128) rescore_touched<2, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
+        else rescore_touched<kMaxTouchedSlots, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
+    }
+    if (ST) { asm volatile("" ::"v"(tk), "v"(ti), "v"(ts)); t1 = stamp(); }
+    // candidate list: valid prefix, first entry not committed in this batch
+    const bool valid = lane < K && my.idx != kNoIdx;
+    const bool untouched = valid && (cx.nT == 0 || !touched_has(cx, my.idx));
+    const uint64_t vmask = __ballot(valid);
+    const uint64_t umask = __ballot(untouched);
+    const int cv = __popcll(vmask);
+    const int uq = umask ? __ffsll((unsigned long long)umask) - 1 : K;
+    if (cx.nT > 0) wave_argbest_fast(tk, ti, ts);
+    if (ST) { asm volatile("" ::"v"(tk), "v"(ti), "v"(ts)); t2 = stamp(); }
+    const int64_t fc = ps.fc0 + df;
+    int32_t oidx = -1;
+    double osc = 0.0;
+    int kind = 0;  // 0 none, 1 winner from list (new touch), 2 winner already touched, 3 overflow
+    double wk = 0.0;
+    int32_t wi = kNoIdx;
+    if (fc != 0) {
+        if (uq < cv) {
+            const double uk = readlane_f64(my.key, uq);
+            const int32_t ui = __builtin_amdgcn_readlane(my.idx, uq);
+            if (ti != kNoIdx && better(tk, ti, uk, ui)) { kind = 2; wk = tk; wi = ti; }
+            else { kind = 1; wk = uk; wi = ui; }
+        } else if (cv < K) {
+            if (ti != kNoIdx) { kind = 2; wk = tk; wi = ti; }
+        } else {
+            const double lk = readlane_f64(my.key, K - 1);
+            const int32_t li = __builtin_amdgcn_readlane(my.idx, K - 1);
+            if (ti != kNoIdx && better(tk, ti, lk, li)) { kind = 2; wk = tk; wi = ti; }
+            else kind = 3;
+        }
+    }
+    if (ST) t3 = stamp();
+    if (kind == 3) return true;  // overflow: stop before pod i (wave-uniform)
+    if (fc != 0) {
+        if (kind == 0) {
+            oidx = -2;
+        } else {
+            oidx = wi;
+            osc = PRIO == kPrioPrice ? -wk : wk;
+            ++cx.placed;
+            int slot = ts;
+            int writer = 0;
+            int64_t b0, b1, b2;
+            if (kind == 1) {  // first touch: the holder of the candidate opens the slot
+                slot = cx.nT++;
+                writer = uq;
+                b0 = my.a[0]; b1 = my.a[1]; b2 = my.a[2];
+                if (lane == uq) {
+                    Touched &x = cx.T[slot];
+                    x.idx = my.idx; x.mine = 1;
+                    x.s0[0] = b0; x.s0[1] = b1; x.s0[2] = b2;
+                    x.sb[0] = b0; x.sb[1] = b1; x.sb[2] = b2;  // untouched by the previous batch
+                    x.labels = my.labels; x.price = my.price; x.pad2 = 0;
+                    touched_insert(cx, my.idx);
+                }
+            } else {
+                b0 = cx.T[slot].cur[0]; b1 = cx.T[slot].cur[1]; b2 = cx.T[slot].cur[2];
+            }
+            if (lane == writer) {
+                Touched &x = cx.T[slot];
+                x.mine = 1;
+                const int64_t c0 = wsub(b0, rc), c1 = wsub(b1, rm), c2 = wsub(b2, 1);
+                x.cur[0] = c0; x.cur[1] = c1; x.cur[2] = c2;
+                x.curf[0] = (double)c0; x.curf[1] = (double)c1; x.curf[2] = (double)c2;
+                x.cury[0] = recip_or_zero(c0, x.curf[0]);
+                x.cury[1] = recip_or_zero(c1, x.curf[1]);
+                x.cury[2] = recip_or_zero(c2, x.curf[2]);
+            }
+        }
+    }
+    if (lane == 0) {
+        const int64_t pod = cx.p0 + i;
+        A.out.idx[pod] = oidx;
+        A.out.score[pod] = osc;
+        A.out.feas[pod] = (int32_t)fc;
+    }
+    if (ST) {
+        const uint64_t t4 = stamp();
+        ph[0] += t1 - t0; ph[1] += t2 - t1; ph[2] += t3 - t2; ph[3] += t4 - t3;
+    }
+    return false;
+}
+
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool ST>
+__device__ __forceinline__ int commit_loop(const CommitArgs &A, CommitCtx &cx, int nb, uint64_t *ph) {
+    // pod i+1's staged request and candidates are read from LDS while pod i is being decided
+    PodStage ps = cx.PS[0];
+    CandStage my;
+    if (cx.lane < K) my = cx.CS[cx.lane];
+    else { my.idx = kNoIdx; my.key = -__builtin_inf(); }
+    for (int i = 0; i < nb; ++i) {
+        PodStage ps_n = ps;
+        CandStage my_n = my;
+        if (i + 1 < nb) {
+            ps_n = cx.PS[i + 1];
+            if (cx.lane < K) my_n = cx.CS[(i + 1) * K + cx.lane];
+        }
+        if (commit_step<K, PRIO, DOM, LAB, F53, ST>(A, cx, i, ps, my, ph)) return i;
+        ps = ps_n;
+        my = my_n;
+    }
+    return nb;
+}
+
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint32_t *bitmap = reinterpret_cast<uint32_t *>(smem);
-    Touched *T = reinterpret_cast<Touched *>(smem + (size_t)A.bitmap_words * 4);
-    PodStage *PS = reinterpret_cast<PodStage *>(smem + (size_t)A.bitmap_words * 4 + (size_t)A.B * sizeof(Touched));
     const int lane = threadIdx.x;
-    const int64_t p0 = *A.cursor;
-    if (p0 >= A.pods.p) return;
+    const int64_t p0 = *A.plan;
+    const int64_t cursor = A.ctl->cursor;
+    if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
+        // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
+        if (lane == 0) {
+            A.xout->count = 0;
+            if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
+        }
+        return;
+    }
+    CommitCtx cx;
+    cx.hkey = reinterpret_cast<int32_t *>(smem);
+    char *p = smem + kTouchHash * sizeof(int32_t);
+    cx.filt = reinterpret_cast<uint32_t *>(p);
+    p += kTouchFilterWords * sizeof(uint32_t);
+    cx.T = reinterpret_cast<Touched *>(p);
+    p += (size_t)2 * A.B * sizeof(Touched);
+    PodStage *PS = reinterpret_cast<PodStage *>(p);
+    p += (size_t)A.B * sizeof(PodStage);
+    CandStage *CS = reinterpret_cast<CandStage *>(p);
+    cx.PS = PS;
+    cx.CS = CS;
+    cx.lane = lane;
+    cx.placed = 0;
+    cx.p0 = p0;
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);
-    for (int w = lane; w < A.bitmap_words; w += 64) bitmap[w] = 0;
+    cx.y3 = recip(3.0);
+    for (int w = lane; w < kTouchHash; w += 64) cx.hkey[w] = -1;
+    for (int w = lane; w < kTouchFilterWords; w += 64) cx.filt[w] = 0;
     for (int b = lane; b < nb; b += 64) {
         PodStage s;
         s.rc = A.pods.rc[p0 + b]; s.rm = A.pods.rm[p0 + b]; s.rp = A.pods.rp[p0 + b];
@@ -488,113 +596,97 @@ __global__ __launch_bounds__(64) void k_commit1(CommitArgs A) {
         s.fc0 = A.fc0[b];
         PS[b] = s;
     }
-    Rec nxt;
-    if (lane < K) nxt = A.lists[lane];
-    else { nxt.valid = 0; nxt.idx = kNoIdx; nxt.key = -__builtin_inf(); }
-    __syncthreads();  // one wave: orders the staging writes before the loop's reads
-
-    int nT = 0;
-    int done = nb;
-    int64_t placed = 0;
-    for (int i = 0; i < nb; ++i) {
-        const Rec my = nxt;
-        if (lane < K && i + 1 < nb) nxt = A.lists[(size_t)(i + 1) * K + lane];
-        const PodStage ps = PS[i];
-        const int64_t rc = ps.rc, rm = ps.rm, rp = ps.rp;
-        const uint64_t sel = ps.sel;
-        const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
-        // re-score the nodes already committed in this batch
-        int64_t df = 0;
-        double tk = -__builtin_inf();
-        int32_t ti = kNoIdx, ts = -1;
-        for (int t = lane; t < nT; t += 64) {
-            const Touched &x = T[t];
-            const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
-            const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
-            df += (int64_t)f1 - (int64_t)f0;
-            double k;
-            if (pair_key<PRIO, DOM>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2], (double)x.cur[0],
-                                    (double)x.cur[1], (double)x.cur[2], x.price, &k) &&
-                better(k, x.idx, tk, ti)) {
-                tk = k; ti = x.idx; ts = t;
-            }
-        }
-        // candidate list: valid prefix, first entry not committed in this batch
-        const bool valid = lane < K && my.valid;
-        const bool untouched = valid && !(bitmap[(uint32_t)my.idx >> 5] & (1u << ((uint32_t)my.idx & 31)));
-        const uint64_t vmask = __ballot(valid);
-        const uint64_t umask = __ballot(untouched);
-        const int cv = __popcll(vmask);
-        const int uq = umask ? __ffsll((unsigned long long)umask) - 1 : K;
-        wave_argbest(tk, ti, ts);
-        df = wave_sum_i64(df);
-        const int64_t fc = ps.fc0 + df;
-        int32_t oidx = -1;
-        double osc = 0.0;
-        int kind = 0;  // 0 none, 1 winner from list (new touch), 2 winner already touched, 3 overflow
-        double wk = 0.0;
-        int32_t wi = kNoIdx;
-        if (fc != 0) {
-            if (uq < cv) {
-                const double uk = __shfl(my.key, uq, 64);
-                const int32_t ui = __shfl(my.idx, uq, 64);
-                if (ti != kNoIdx && better(tk, ti, uk, ui)) { kind = 2; wk = tk; wi = ti; }
-                else { kind = 1; wk = uk; wi = ui; }
-            } else if (cv < K) {
-                if (ti != kNoIdx) { kind = 2; wk = tk; wi = ti; }
-            } else {
-                const double lk = __shfl(my.key, K - 1, 64);
-                const int32_t li = __shfl(my.idx, K - 1, 64);
-                if (ti != kNoIdx && better(tk, ti, lk, li)) { kind = 2; wk = tk; wi = ti; }
-                else kind = 3;
-            }
-        }
-        if (kind == 3) { done = i; break; }  // wave-uniform
-        if (fc != 0) {
-            if (kind == 0) {
-                oidx = -2;
-            } else {
-                oidx = wi;
-                osc = PRIO == kPrioPrice ? -wk : wk;
-                ++placed;
-                if (kind == 1) {
-                    if (lane == uq) {  // first touch: the holder of the candidate opens the slot
-                        Touched &x = T[nT];
-                        x.idx = my.idx; x.pad = 0;
-                        x.s0[0] = my.a[0]; x.s0[1] = my.a[1]; x.s0[2] = my.a[2];
-                        x.cur[0] = wsub(my.a[0], rc); x.cur[1] = wsub(my.a[1], rm); x.cur[2] = wsub(my.a[2], 1);
-                        x.labels = my.labels; x.price = my.price; x.pad2 = 0;
-                        bitmap[(uint32_t)my.idx >> 5] |= 1u << ((uint32_t)my.idx & 31);
-                    }
-                    ++nT;
-                } else if (lane == 0) {
-                    Touched &x = T[ts];
-                    x.cur[0] = wsub(x.cur[0], rc); x.cur[1] = wsub(x.cur[1], rm); x.cur[2] = wsub(x.cur[2], 1);
-                }
-            }
-        }
-        if (lane == 0) {
-            const int64_t pod = p0 + i;
-            A.out.idx[pod] = oidx;
-            A.out.score[pod] = osc;
-            A.out.feas[pod] = (int32_t)fc;
-        }
+    for (int e = lane; e < nb * K; e += 64) {
+        const Rec r = A.lists[e];
+        CandStage c;
+        c.key = r.key; c.idx = r.valid ? r.idx : kNoIdx; c.price = r.price;
+        c.a[0] = r.a[0]; c.a[1] = r.a[1]; c.a[2] = r.a[2]; c.labels = r.labels;
+        CS[e] = c;
     }
     __syncthreads();
-    for (int t = lane; t < nT; t += 64) {
-        const Touched &x = T[t];
-        const int64_t j = (int64_t)x.idx - A.node_lo;
-        if (j >= 0 && j < A.n_local) {
-            NodeRec *nd = A.nodes + j;
-            nd->a[0] = x.cur[0]; nd->a[1] = x.cur[1]; nd->a[2] = x.cur[2];
-            nd->af[0] = (double)x.cur[0]; nd->af[1] = (double)x.cur[1]; nd->af[2] = (double)x.cur[2];
+    // inherit the nodes the previous batch committed: this batch was scored before those commits
+    const int nin = A.xin->count;
+    for (int e = lane; e < nin; e += 64) {
+        const XRec &xi = A.xin->e[e];
+        Touched &x = cx.T[e];
+        x.idx = xi.idx; x.mine = 0;
+        for (int r = 0; r < 3; ++r) {
+            x.s0[r] = xi.sb[r];
+            x.sb[r] = xi.cur[r];
+            x.cur[r] = xi.cur[r];
+            x.curf[r] = (double)xi.cur[r];
+            x.cury[r] = recip_or_zero(xi.cur[r], x.curf[r]);
         }
+        x.labels = xi.labels; x.price = xi.price; x.pad2 = 0;
+        uint32_t h = thash(xi.idx);
+        while (atomicCAS(&cx.hkey[h], -1, xi.idx) != -1) h = (h + 1) & (kTouchHash - 1);
+        atomicOr(&cx.filt[((uint32_t)xi.idx & 0xffffu) >> 5], 1u << ((uint32_t)xi.idx & 31));
+    }
+    cx.nT = nin;
+    __syncthreads();
+
+    uint64_t ph[4] = {0, 0, 0, 0};
+    int done;
+    if (A.dbg) {
+        const uint64_t tl0 = stamp();
+        done = commit_loop<K, PRIO, DOM, LAB, F53, true>(A, cx, nb, ph);
+        const uint64_t tl1 = stamp();
+        if (lane == 0) {
+            A.dbg[0] += ph[0]; A.dbg[1] += ph[1]; A.dbg[2] += ph[2]; A.dbg[3] += ph[3];
+            A.dbg[4] += tl1 - tl0; A.dbg[5] += done; A.dbg[6] += cx.nT; A.dbg[7] += 1;
+        }
+    } else {
+        done = commit_loop<K, PRIO, DOM, LAB, F53, false>(A, cx, nb, ph);
+    }
+    __syncthreads();
+    // export this batch's commits (wave-ordered compaction)
+    int base = 0;
+    for (int t0 = 0; t0 < cx.nT; t0 += 64) {
+        const int t = t0 + lane;
+        const bool m = t < cx.nT && cx.T[t].mine;
+        const uint64_t mask = __ballot(m);
+        if (m) {
+            const Touched &x = cx.T[t];
+            XRec &o = A.xout->e[base + __popcll(mask & ((1ull << lane) - 1))];
+            o.idx = x.idx; o.pad = 0;
+            o.sb[0] = x.sb[0]; o.sb[1] = x.sb[1]; o.sb[2] = x.sb[2];
+            o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
+            o.labels = x.labels; o.price = x.price; o.pad2 = 0;
+        }
+        base += __popcll(mask);
     }
     if (lane == 0) {
-        *A.cursor = p0 + done;
-        A.stats[0] += 1;
-        A.stats[1] += (done < nb) ? 1 : 0;
-        A.stats[2] += placed;
+        A.xout->count = base;
+        A.ctl->cursor = p0 + done;
+        if (done < nb) A.ctl->resync = 1;
+        A.ctl->stats[0] += 1;
+        A.ctl->stats[1] += (done < nb) ? 1 : 0;
+        A.ctl->stats[2] += cx.placed;
+    }
+}
+
+// Plan the next speculative batch: restart at the committed frontier after a truncation, else
+// continue one full batch after the previous plan.
+__global__ void k_plan(Ctl *ctl, int slot, int B, int64_t P) {
+    if (threadIdx.x != 0) return;
+    int64_t start;
+    if (ctl->resync) {
+        start = ctl->cursor;
+        ctl->resync = 0;
+    } else {
+        start = ctl->spec_next;
+    }
+    ctl->spec_next = start + B;
+    ctl->plan[slot] = start < P ? start : -1;
+}
+
+// Write one batch's committed nodes into this rank's node rows.
+__global__ void k_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local) {
+    const int n = x->count;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const XRec &r = x->e[e];
+        const int64_t j = (int64_t)r.idx - node_lo;
+        if (j >= 0 && j < n_local) set_node(nodes + j, r.cur[0], r.cur[1], r.cur[2]);
     }
 }
 
@@ -605,11 +697,17 @@ __global__ void k_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_
         const int64_t j = idx[i];
         if (j < 0 || j >= n) continue;
         NodeRec *nd = nodes + j;
-        for (int r = 0; r < 3; ++r) {
-            nd->a[r] = (int64_t)((uint64_t)nd->a[r] + (uint64_t)d[r * k + i]);
-            nd->af[r] = (double)nd->a[r];
-        }
+        set_node(nd, (int64_t)((uint64_t)nd->a[0] + (uint64_t)d[i]), (int64_t)((uint64_t)nd->a[1] + (uint64_t)d[k + i]),
+                 (int64_t)((uint64_t)nd->a[2] + (uint64_t)d[2 * k + i]));
     }
+}
+
+__global__ void k_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i], y = b[i];
+    native[i] = x / y;
+    fast[i] = qdiv(x, y, recip(y));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -617,9 +715,9 @@ __global__ void k_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_
 // ------------------------------------------------------------------------------------------------
 namespace {
 
-template <int NPT, int PRIO, int DOM, bool LAB>
+template <int NPT, int PRIO, int DOM, bool LAB, bool F53>
 hipError_t exact_one(const ExactArgs &a, int block, bool coop, hipStream_t s) {
-    auto fn = k_exact<NPT, PRIO, DOM, LAB>;
+    auto fn = k_exact<NPT, PRIO, DOM, LAB, F53>;
     if (coop && a.G > 1) {
         ExactArgs copy = a;
         void *args[] = {&copy};
@@ -629,31 +727,30 @@ hipError_t exact_one(const ExactArgs &a, int block, bool coop, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int PRIO, int DOM, bool LAB>
+template <int PRIO, int DOM, bool LAB, bool F53>
 hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStream_t s) {
     switch (npt) {
-        case 1: return exact_one<1, PRIO, DOM, LAB>(a, block, coop, s);
-        case 2: return exact_one<2, PRIO, DOM, LAB>(a, block, coop, s);
-        case 4: return exact_one<4, PRIO, DOM, LAB>(a, block, coop, s);
-        case 8: return exact_one<8, PRIO, DOM, LAB>(a, block, coop, s);
-        case 16: return exact_one<16, PRIO, DOM, LAB>(a, block, coop, s);
+        case 1: return exact_one<1, PRIO, DOM, LAB, F53>(a, block, coop, s);
+        case 2: return exact_one<2, PRIO, DOM, LAB, F53>(a, block, coop, s);
+        case 4: return exact_one<4, PRIO, DOM, LAB, F53>(a, block, coop, s);
+        case 8: return exact_one<8, PRIO, DOM, LAB, F53>(a, block, coop, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-template <int K, int PRIO, int DOM, bool LAB>
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
 hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
     dim3 grid((a.n_chunks + 3) / 4, pod_groups);
-    hipLaunchKernelGGL((k_score_topk<K, PRIO, DOM, LAB>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_score_topk<K, PRIO, DOM, LAB, F53>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-template <int PRIO, int DOM, bool LAB>
+template <int PRIO, int DOM, bool LAB, bool F53>
 hipError_t score_k(int K, const ScoreArgs &a, int pg, hipStream_t s) {
     switch (K) {
-        case 4: return score_one<4, PRIO, DOM, LAB>(a, pg, s);
-        case 8: return score_one<8, PRIO, DOM, LAB>(a, pg, s);
-        case 16: return score_one<16, PRIO, DOM, LAB>(a, pg, s);
+        case 4: return score_one<4, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 8: return score_one<8, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 16: return score_one<16, PRIO, DOM, LAB, F53>(a, pg, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -672,54 +769,70 @@ hipError_t merge_k(bool rec, bool fin, const MergeArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int K, int PRIO, int DOM, bool LAB>
-hipError_t commit_one(const CommitArgs &a, size_t lds, bool single_wave, hipStream_t s) {
-    static bool attr_set[2] = {false, false};
-    const void *fn = single_wave ? (const void *)k_commit1<K, PRIO, DOM, LAB> : (const void *)k_commit<K, PRIO, DOM, LAB>;
-    if (!attr_set[single_wave]) {
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t commit_one(const CommitArgs &a, size_t lds, hipStream_t s) {
+    static bool attr_set = false;
+    const void *fn = (const void *)k_commit<K, PRIO, DOM, LAB, F53>;
+    if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
         if (e != hipSuccess) return e;
-        attr_set[single_wave] = true;
+        attr_set = true;
     }
-    if (single_wave) hipLaunchKernelGGL((k_commit1<K, PRIO, DOM, LAB>), dim3(1), dim3(64), lds, s, a);
-    else hipLaunchKernelGGL((k_commit<K, PRIO, DOM, LAB>), dim3(1), dim3(kCommitBlock), lds, s, a);
+    hipLaunchKernelGGL((k_commit<K, PRIO, DOM, LAB, F53>), dim3(1), dim3(64), lds, s, a);
     return hipGetLastError();
 }
 
-template <int PRIO, int DOM, bool LAB>
-hipError_t commit_k(int K, const CommitArgs &a, size_t lds, bool sw, hipStream_t s) {
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t commit_k(int K, const CommitArgs &a, size_t lds, hipStream_t s) {
     switch (K) {
-        case 4: return commit_one<4, PRIO, DOM, LAB>(a, lds, sw, s);
-        case 8: return commit_one<8, PRIO, DOM, LAB>(a, lds, sw, s);
-        case 16: return commit_one<16, PRIO, DOM, LAB>(a, lds, sw, s);
+        case 4: return commit_one<4, PRIO, DOM, LAB, F53>(a, lds, s);
+        case 8: return commit_one<8, PRIO, DOM, LAB, F53>(a, lds, s);
+        case 16: return commit_one<16, PRIO, DOM, LAB, F53>(a, lds, s);
         default: return hipErrorInvalidValue;
     }
 }
 
-// (priority, domain, labels) -> instantiation.  Best-price always ranges over feasible nodes.
-#define KSCHED_DISPATCH(prio, dom, lab, CALL)                                   \
-    do {                                                                        \
-        if ((prio) == kPrioPrice) {                                             \
-            if (lab) { constexpr int P_ = kPrioPrice, D_ = kDomFeasible; constexpr bool L_ = true; return CALL; } \
-            else { constexpr int P_ = kPrioPrice, D_ = kDomFeasible; constexpr bool L_ = false; return CALL; }    \
-        } else if ((dom) == kDomFeasible) {                                     \
-            if (lab) { constexpr int P_ = kPrioResource, D_ = kDomFeasible; constexpr bool L_ = true; return CALL; } \
-            else { constexpr int P_ = kPrioResource, D_ = kDomFeasible; constexpr bool L_ = false; return CALL; }    \
-        } else {                                                                \
-            if (lab) { constexpr int P_ = kPrioResource, D_ = kDomAll; constexpr bool L_ = true; return CALL; }      \
-            else { constexpr int P_ = kPrioResource, D_ = kDomAll; constexpr bool L_ = false; return CALL; }         \
-        }                                                                       \
+// (priority, domain, labels, fast53) -> instantiation.  Best-price always ranges over feasible nodes
+// and never divides (fast53 irrelevant).
+#define KSCHED_DISPATCH(prio, dom, lab, f53, CALL)                                              \
+    do {                                                                                        \
+        if ((prio) == kPrioPrice) {                                                             \
+            constexpr int P_ = kPrioPrice, D_ = kDomFeasible; constexpr bool F_ = false;        \
+            if (lab) { constexpr bool L_ = true; return CALL; }                                 \
+            else { constexpr bool L_ = false; return CALL; }                                    \
+        }                                                                                       \
+        constexpr int P_ = kPrioResource;                                                       \
+        if ((dom) == kDomFeasible) {                                                            \
+            constexpr int D_ = kDomFeasible;                                                    \
+            if (lab) { constexpr bool L_ = true;                                                \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+            else { constexpr bool L_ = false;                                                   \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+        } else {                                                                                \
+            constexpr int D_ = kDomAll;                                                         \
+            if (lab) { constexpr bool L_ = true;                                                \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+            else { constexpr bool L_ = false;                                                   \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+        }                                                                                       \
     } while (0)
 
 }  // namespace
 
-hipError_t launch_exact(int npt, int prio, int dom, bool lab, const ExactArgs &a, int block, bool coop,
-                        hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, (exact_npt<P_, D_, L_>(npt, a, block, coop, s)));
+hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_prep_nodes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n);
+    return hipGetLastError();
 }
 
-hipError_t launch_score_topk(int K, int prio, int dom, bool lab, const ScoreArgs &a, int pod_groups, hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, (score_k<P_, D_, L_>(K, a, pod_groups, s)));
+hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool f53, const ExactArgs &a, int block, bool coop,
+                        hipStream_t s) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (exact_npt<P_, D_, L_, F_>(npt, a, block, coop, s)));
+}
+
+hipError_t launch_score_topk(int K, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,
+                             hipStream_t s) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(K, a, pod_groups, s)));
 }
 
 hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s) {
@@ -731,14 +844,31 @@ hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs
     }
 }
 
-hipError_t launch_commit(int K, int prio, int dom, bool lab, const CommitArgs &a, size_t lds_bytes, bool single_wave,
+hipError_t launch_commit(int K, int prio, int dom, bool lab, bool f53, const CommitArgs &a, size_t lds_bytes,
                          hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, (commit_k<P_, D_, L_>(K, a, lds_bytes, single_wave, s)));
+    KSCHED_DISPATCH(prio, dom, lab, f53, (commit_k<P_, D_, L_, F_>(K, a, lds_bytes, s)));
 }
 
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_apply_delta, dim3(1), dim3(64), 0, s, nodes, n, k, idx, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan(Ctl *ctl, int slot, int B, int64_t P, hipStream_t s) {
+    hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, ctl, slot, B, P);
+    return hipGetLastError();
+}
+
+hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s) {
+    hipLaunchKernelGGL(k_apply_batch, dim3(1), dim3(256), 0, s, x, nodes, node_lo, n_local);
+    return hipGetLastError();
+}
+
+hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,
+                               hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_selftest_div, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a, b, native, fast);
     return hipGetLastError();
 }
 

@@ -97,7 +97,7 @@ def test_exact_mode_workgroup_counts(gpu_available, oracle_mod):
     cl = cluster.make_cluster("c3", n_nodes=6000, n_pods=600)
     want = oracle_mod.schedule(cl, nthreads=8)
     for g in (1, 2, 3, 7, 24, 64, 200):
-        if 6000 > g * 256 * 16:
+        if 6000 > g * 256 * 8:
             continue
         assert_same(run_engine(cl, MODE_EXACT, exact_wgs=g), want, f"G={g}")
 
@@ -168,3 +168,77 @@ def test_full_size_c3_batched_equals_exact(gpu_available):
     assert np.array_equal(a[3][0], exp_c) and np.array_equal(a[3][1], exp_m) and np.array_equal(a[3][2], exp_p)
     # the committed pods' recorded scores are positive (only s > 0 can win)
     assert (a[1][placed] > 0).all()
+
+
+def test_hoisted_reciprocal_division_is_bit_exact(gpu_available):
+    """qdiv(a, b, recip(b)) == hipcc's a / b, bit for bit, over the operand classes of the score:
+    integer-valued numerators/divisors across magnitudes and signs (incl. > 2^53 and near 2^63),
+    the /3 of sums of fractions and of squared deviations, and the *10 least-requested numerators."""
+    import ctypes as C
+    from ksched import Engine
+    from ksched import _lib as L
+    rng = np.random.default_rng(11)
+    n = 1 << 21
+    mags = rng.integers(0, 63, size=n)
+    ai = (rng.integers(0, 1 << 62, size=n, dtype=np.int64) >> (62 - np.minimum(mags, 62))).astype(np.int64)
+    ai[rng.random(n) < 0.3] *= -1
+    bi = (rng.integers(1, 1 << 62, size=n, dtype=np.int64) >> (62 - np.minimum(rng.integers(0, 63, size=n), 62))).astype(np.int64)
+    bi[bi == 0] = 1
+    bi[rng.random(n) < 0.3] *= -1
+    a = ai.astype(np.float64)
+    b = bi.astype(np.float64)
+    # fraction-like numerators over 3.0
+    k = n // 4
+    fr = (rng.integers(1, 1 << 40, size=k) / rng.integers(1, 1 << 50, size=k).astype(np.float64))
+    a[:k] = fr + fr[::-1] + (fr * fr)
+    b[:k] = 3.0
+    # tiny squared deviations over 3.0
+    a[k:2 * k] = (fr - fr[::-1]) ** 2
+    b[k:2 * k] = 3.0
+    # least-requested numerators: (cap - req) * 10 over cap
+    cap = rng.integers(1, 1 << 45, size=k).astype(np.int64)
+    req = rng.integers(0, 1 << 45, size=k).astype(np.int64) % cap
+    a[2 * k:3 * k] = (cap - req).astype(np.float64) * 10.0
+    b[2 * k:3 * k] = cap.astype(np.float64)
+    native = np.empty(n); fast = np.empty(n)
+    with Engine() as e:
+        rc = L.lib().ksched_selftest_fastdiv(e._ctx, n, L.ptr(a, C.c_double), L.ptr(b, C.c_double),
+                                             L.ptr(native, C.c_double), L.ptr(fast, C.c_double))
+        assert rc == 0
+    # nonzero numerators: identical bits; zero numerators: identical value (signed zero may differ,
+    # and never reaches a score -- DESIGN.md)
+    nz = a != 0
+    bad = np.nonzero(native[nz].view(np.int64) != fast[nz].view(np.int64))[0]
+    assert bad.size == 0, f"{bad.size} mismatches, e.g. {a[nz][bad[:3]]}/{b[nz][bad[:3]]}"
+    assert np.array_equal(native[~nz], fast[~nz])
+    # and both equal the correctly rounded CPU quotient
+    assert np.array_equal(native[nz].view(np.int64), (a[nz] / b[nz]).view(np.int64))
+
+
+def test_collective_path_one_rank(gpu_available, oracle_mod):
+    """The node-sharded path (RCCL all-gather of the local candidate records + rank merge) on a 1-rank
+    communicator: same bits as the oracle.  Exercises ksched_get_unique_id / ksched_set_comm,
+    ncclAllGather inside the engine and k_merge<INPUT_REC>."""
+    from ksched import Engine, MODE_BATCHED, cluster
+    for name, nn, pp, K in (("c3", 20000, 1500, 16), ("c5", 30000, 1500, 8), ("c2", 5000, 1500, 4)):
+        cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+        want = oracle_mod.schedule(cl, nthreads=8)
+        with Engine(mode=MODE_BATCHED, priority=cl.priority, domain=cl.domain, use_labels=cl.use_labels,
+                    topk=K, batch=8 * K, nranks=1, nodes_global=cl.n_nodes) as e:
+            e.set_comm(Engine.unique_id())
+            e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods, labels=cl.labels, price=cl.price)
+            oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+            st = e.read_nodes()
+        assert_same((oi, os_, of, st), want, f"{name}/collective")
+
+
+def test_sharded_engine_helper_world1(gpu_available, oracle_mod):
+    from ksched import cluster
+    from ksched.dist import make_sharded_engine
+    cl = cluster.make_cluster("c3", n_nodes=8000, n_pods=800)
+    eng, (lo, hi) = make_sharded_engine(cl, 0, 1, device=0, topk=8, batch=64)
+    assert (lo, hi) == (0, 8000)
+    oi, os_, of = eng.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+    st = eng.read_nodes()
+    eng.close()
+    assert_same((oi, os_, of, st), oracle_mod.schedule(cl), "sharded-helper")
