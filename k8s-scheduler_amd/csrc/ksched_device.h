@@ -149,6 +149,38 @@ __device__ __forceinline__ bool pair_key_fast(bool feas, int64_t rc, int64_t rm,
 
 __device__ __forceinline__ double recip_or_zero(int64_t a, double af) { return a == 0 ? 0.0 : recip(af); }
 
+// Upper bound of the resource score without the division corrections: every a / b is replaced by
+// a * recip(b) (relative error <= 2^-51 per quotient), so |approx - exact| <= ~1e3 * 2^-52 *
+// (|balanced| + |least| + 20); the bound adds 1e-9 * (|balanced| + |least| + 1), orders of magnitude
+// more.  *near1 flags a fraction within 1e-12 of 1, where the balanced branch (fraction >= 1) could
+// differ from the exact one -- such pairs must be scored exactly.
+template <bool FAST53>
+__device__ __forceinline__ double resource_score_upper(int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,
+                                                       double rpf, int64_t ac, int64_t am, int64_t ap, double acf,
+                                                       double amf, double apf, double yc, double ym, double yp,
+                                                       double y3, bool *near1) {
+    const double c = (ac == 0) ? 1.0 : rcf * yc;
+    const double m = (am == 0) ? 1.0 : rmf * ym;
+    const double p = (ap == 0) ? 1.0 : rpf * yp;
+    *near1 = (ac != 0 && __builtin_fabs(c - 1.0) < 1e-12) | (am != 0 && __builtin_fabs(m - 1.0) < 1e-12) |
+             (ap != 0 && __builtin_fabs(p - 1.0) < 1e-12);
+    double b = 0.0;
+    if (!(c >= 1.0 || m >= 1.0 || p >= 1.0)) {
+        const double mean = ((c + m) + p) * y3;
+        const double var = (((c - mean) * (c - mean) + (m - mean) * (m - mean)) + (p - mean) * (p - mean)) * y3;
+        b = (1.0 - var) * 10.0;
+    }
+    const double dc = FAST53 ? acf - rcf : (double)wsub(ac, rc);
+    const double dm = FAST53 ? amf - rmf : (double)wsub(am, rm);
+    const double dp = FAST53 ? apf - rpf : (double)wsub(ap, rp);
+    const double lc = (ac == 0 || rc > ac) ? 0.0 : dc * 10.0 * yc;
+    const double lm = (am == 0 || rm > am) ? 0.0 : dm * 10.0 * ym;
+    const double lp = (ap == 0 || rp > ap) ? 0.0 : dp * 10.0 * yp;
+    const double l = ((lc + lm) + lp) * y3;
+    const double s = (b + l) * 0.5;
+    return s + 1e-9 * (__builtin_fabs(b) + __builtin_fabs(l) + 1.0);
+}
+
 // The resource score of one (request, allocatable) pair.  rcf/... are (double) of the int64 values
 // (hoisted by callers; (double)int64 is correctly rounded, identical wherever it is computed).
 __device__ __forceinline__ double resource_score(int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,

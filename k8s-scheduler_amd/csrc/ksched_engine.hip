@@ -472,6 +472,10 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
         ksched_destroy(c);
         return KSCHED_E_DEVICE;
     }
+    if (hipMemset(c->d_err, 0, sizeof(int32_t)) != hipSuccess) {  // error word read by every sync
+        ksched_destroy(c);
+        return KSCHED_E_DEVICE;
+    }
     *out = c;
     return KSCHED_OK;
 }

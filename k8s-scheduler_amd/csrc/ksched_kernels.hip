@@ -230,20 +230,22 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
         const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
         cnt += f;
         double k;
+        // Nodes arrive in ascending index, so a newcomer loses every tie: a strict key compare keeps
+        // the list in (key desc, idx asc) order (empty slots hold -inf and never beat a real key).
         if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1], nd.af[2],
-                                          nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k)) {
+                                          nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k) &&
+            k > key[K - 1]) {
+            double ck = k;
             int32_t ci = (int32_t)(A.node_offset + j);
-            if (better(k, ci, key[K - 1], idx[K - 1])) {
-                double ck = k;
+            bool moved = false;  // once placed, every later entry shifts down one slot
 #pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    if (better(ck, ci, key[q], idx[q])) {
-                        const double tk = key[q];
-                        const int32_t ti = idx[q];
-                        key[q] = ck; idx[q] = ci;
-                        ck = tk; ci = ti;
-                    }
-                }
+            for (int q = 0; q < K; ++q) {
+                const bool sw = moved || ck > key[q];
+                moved = sw;
+                const double tk = key[q];
+                const int32_t ti = idx[q];
+                key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+                ck = sw ? tk : ck; ci = sw ? ti : ci;
             }
         }
     }
@@ -384,12 +386,15 @@ __device__ __forceinline__ void touched_insert(CommitCtx &cx, int32_t idx) {
     cx.filt[((uint32_t)idx & 0xffffu) >> 5] |= 1u << ((uint32_t)idx & 31);
 }
 
-// Re-score NS touched slots per lane (t = lane + 64 s), branch-free so the NS dependency chains
-// interleave; feasibility deltas through ballots.
+// Touched-node re-scoring, filtered: an upper bound (reciprocal multiplies, no corrections) per slot
+// decides which touched nodes could beat the threshold (thk, thi); only those are scored exactly.
+// Non-candidates provably rank below the threshold, so the decision is unchanged.
+// Feasibility deltas (exact integer compares) come through ballots.
 template <int NS, int PRIO, int DOM, bool LAB, bool F53>
 __device__ __forceinline__ void rescore_touched(const CommitCtx &cx, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
-                                                double rcf, double rmf, double rpf, int64_t &df, double &tk,
-                                                int32_t &ti, int32_t &ts) {
+                                                double rcf, double rmf, double rpf, double thk, int32_t thi,
+                                                int64_t &df, double &tk, int32_t &ti, int32_t &ts, bool &any) {
+    bool cand[NS];
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
         const int t = cx.lane + 64 * s;
@@ -397,12 +402,35 @@ __device__ __forceinline__ void rescore_touched(const CommitCtx &cx, int64_t rc,
         const Touched &x = cx.T[in ? t : 0];
         const bool f0 = in && fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
         const bool f1 = in && fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
-        double k;
-        const bool ok = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
-                                                      x.curf[0], x.curf[1], x.curf[2], x.cury[0], x.cury[1],
-                                                      x.cury[2], cx.y3, x.price, &k);
-        if (in && ok && better(k, x.idx, tk, ti)) { tk = k; ti = x.idx; ts = t; }
         df += (int64_t)__popcll(__ballot(f1)) - (int64_t)__popcll(__ballot(f0));
+        bool c;
+        if (PRIO == kPrioPrice) {
+            c = f1 && better(-(double)x.price, x.idx, thk, thi);
+        } else {
+            bool near1;
+            const double hi = resource_score_upper<F53>(rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
+                                                        x.curf[0], x.curf[1], x.curf[2], x.cury[0], x.cury[1],
+                                                        x.cury[2], cx.y3, &near1);
+            c = in && (DOM == kDomAll || f1) && (near1 || (hi > 0.0 && hi >= thk));
+        }
+        cand[s] = c;
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        if (__ballot(cand[s]) == 0) continue;  // wave-uniform: nothing to score exactly in this slot
+        any = true;
+        if (cand[s]) {
+            const int t = cx.lane + 64 * s;
+            const Touched &x = cx.T[t];
+            const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
+            double k;
+            if (pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2], x.curf[0],
+                                              x.curf[1], x.curf[2], x.cury[0], x.cury[1], x.cury[2], cx.y3, x.price,
+                                              &k) &&
+                better(k, x.idx, tk, ti)) {
+                tk = k; ti = x.idx; ts = t;
+            }
+        }
     }
 }
 
@@ -443,16 +471,6 @@ __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, 
     const int64_t rc = ps.rc, rm = ps.rm, rp = ps.rp;
     const uint64_t sel = ps.sel;
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
-    // re-score the nodes already committed in this batch
-    int64_t df = 0;
-    double tk = -__builtin_inf();
-    int32_t ti = kNoIdx, ts = -1;
-    if (cx.nT > 0) {
-        if (cx.nT <= 64) rescore_touched<1, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
-        else if (cx.nT <= 128) rescore_touched<2, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
-        else rescore_touched<kMaxTouchedSlots, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, df, tk, ti, ts);
-    }
-    if (ST) { asm volatile("" ::"v"(tk), "v"(ti), "v"(ts)); t1 = stamp(); }
     // candidate list: valid prefix, first entry not committed in this batch
     const bool valid = lane < K && my.idx != kNoIdx;
     const bool untouched = valid && (cx.nT == 0 || !touched_has(cx, my.idx));
@@ -460,7 +478,27 @@ __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, 
     const uint64_t umask = __ballot(untouched);
     const int cv = __popcll(vmask);
     const int uq = umask ? __ffsll((unsigned long long)umask) - 1 : K;
-    if (cx.nT > 0) wave_argbest_fast(tk, ti, ts);
+    // threshold a touched node must beat to matter: u*, else list[K-1] (full list), else anything
+    double thk = -__builtin_inf();
+    int32_t thi = kNoIdx;
+    if (uq < cv) { thk = readlane_f64(my.key, uq); thi = __builtin_amdgcn_readlane(my.idx, uq); }
+    else if (cv == K) { thk = readlane_f64(my.key, K - 1); thi = __builtin_amdgcn_readlane(my.idx, K - 1); }
+    // re-score the nodes already committed (this batch's and the previous batch's)
+    int64_t df = 0;
+    double tk = -__builtin_inf();
+    int32_t ti = kNoIdx, ts = -1;
+    bool any = false;
+    if (cx.nT > 0) {
+        if (cx.nT <= 64)
+            rescore_touched<1, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, thk, thi, df, tk, ti, ts, any);
+        else if (cx.nT <= 128)
+            rescore_touched<2, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, thk, thi, df, tk, ti, ts, any);
+        else
+            rescore_touched<kMaxTouchedSlots, PRIO, DOM, LAB, F53>(cx, rc, rm, rp, sel, rcf, rmf, rpf, thk, thi, df, tk,
+                                                                   ti, ts, any);
+    }
+    if (ST) { asm volatile("" ::"v"(tk), "v"(ti), "v"(ts)); t1 = stamp(); }
+    if (any) wave_argbest_fast(tk, ti, ts);
     if (ST) { asm volatile("" ::"v"(tk), "v"(ti), "v"(ts)); t2 = stamp(); }
     const int64_t fc = ps.fc0 + df;
     int32_t oidx = -1;

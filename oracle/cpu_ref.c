@@ -626,3 +626,118 @@ int or_schedule_batched(const or_opts *o, int32_t K, int32_t B, int64_t n,
 
 int or_rec_size(void) { return (int)sizeof(or_rec); }
 int or_touched_size(void) { return (int)sizeof(or_touched); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Pipelined restatement of the GPU batched mode: batch b is scored against */
+/* the node rows as of batch b-2's commits (lag one batch), speculatively planned at the previous */
+/* start + B; commit(b) skips a batch whose planned start is not the committed frontier, inherits */
+/* the nodes committed by batch b-1, and stops at the first candidate-list overflow (resync).    */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct or_xrec { int32_t idx; int64_t sb[3], cur[3]; uint64_t labels; float price; } or_xrec;
+
+static int64_t commit_inherit(const or_opts *o, int32_t K, int64_t nb, const int64_t *rc, const int64_t *rm,
+                              const int64_t *rp, const uint64_t *sel, const or_rec *lists, const int64_t *fc0,
+                              const or_xrec *xin, int32_t nin, or_xrec *xout, int32_t *nout,
+                              int32_t *out_idx, double *out_score, int32_t *out_feas)
+{
+    /* touched table: inherited entries first (s0 = state at this batch's snapshot, cur = current) */
+    or_touched *T = (or_touched *)malloc(sizeof(or_touched) * (size_t)(nin + nb + 1));
+    int32_t *mine = (int32_t *)calloc((size_t)(nin + nb + 1), sizeof(int32_t));
+    int64_t (*sb)[3] = malloc(sizeof(int64_t[3]) * (size_t)(nin + nb + 1));
+    int32_t nt = nin, t;
+    int64_t done;
+    for (t = 0; t < nin; t++) {
+        T[t].idx = xin[t].idx;
+        memcpy(T[t].s0, xin[t].sb, sizeof(T[t].s0));
+        memcpy(T[t].cur, xin[t].cur, sizeof(T[t].cur));
+        memcpy(sb[t], xin[t].cur, sizeof(sb[t]));
+        T[t].labels = xin[t].labels; T[t].price = xin[t].price;
+    }
+    {
+        /* reuse or_commit_batch's decision rule, but with a pre-filled touched table */
+        int32_t before = nt;
+        done = or_commit_batch(o, K, nb, rc, rm, rp, sel, lists, fc0, T, &nt, nin + (int32_t)nb + 1,
+                               out_idx, out_score, out_feas);
+        /* entries opened by this batch: state at batch start = snapshot state */
+        for (t = before; t < nt; t++) memcpy(sb[t], T[t].s0, sizeof(sb[t]));
+    }
+    /* which entries did this batch commit to?  an entry changed iff cur != state at batch start */
+    *nout = 0;
+    for (t = 0; t < nt; t++) {
+        int64_t i;
+        int hit = t >= nin;
+        for (i = 0; !hit && i < done; i++) hit = out_idx[i] == T[t].idx;
+        if (!hit) continue;
+        xout[*nout].idx = T[t].idx;
+        memcpy(xout[*nout].sb, sb[t], sizeof(sb[t]));
+        memcpy(xout[*nout].cur, T[t].cur, sizeof(T[t].cur));
+        xout[*nout].labels = T[t].labels; xout[*nout].price = T[t].price;
+        (*nout)++;
+    }
+    (void)mine;
+    free(T); free(mine); free(sb);
+    return done;
+}
+
+int or_schedule_pipelined(const or_opts *o, int32_t K, int32_t B, int64_t n,
+                          int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
+                          int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
+                          int32_t *out_idx, double *out_score, int32_t *out_feas, int64_t *stats)
+{
+    /* ac/am/ap are the node rows (what score reads); they receive batch b-2's commits before batch b */
+    or_xrec *X[3];
+    int32_t nx[3] = {0, 0, 0};
+    or_rec *recs;
+    int64_t *fc;
+    int64_t cursor = 0, spec_next = 0, b;
+    int resync = 0, k;
+    if (K < 1 || B < 1) return OR_E_INVALID;
+    for (k = 0; k < 3; k++) X[k] = (or_xrec *)malloc(sizeof(or_xrec) * (size_t)(2 * B + 1));
+    recs = (or_rec *)malloc(sizeof(or_rec) * (size_t)K * (size_t)B);
+    fc = (int64_t *)malloc(sizeof(int64_t) * (size_t)B);
+    if (stats) stats[0] = stats[1] = stats[2] = 0;
+    for (b = 0; cursor < p; b++) {
+        int cb = (int)(b % 3), pb = (int)((b + 2) % 3); /* X(b), X(b-1) */
+        int64_t s, nb, done, i;
+        if (b >= 2) { /* apply(b-2) */
+            int ab = (int)((b - 2) % 3);
+            for (i = 0; i < nx[ab]; i++) {
+                int32_t j = X[ab][i].idx;
+                ac[j] = X[ab][i].cur[0]; am[j] = X[ab][i].cur[1]; ap[j] = X[ab][i].cur[2];
+            }
+            nx[ab] = 0;
+        }
+        /* plan(b): sees the commits of batches <= b-2 */
+        if (resync) { s = cursor; resync = 0; } else s = spec_next;
+        spec_next = s + B;
+        /* commit(b-1) happens "concurrently" with score(b): model it after plan(b) */
+        (void)pb;
+        nb = s < p ? (p - s < B ? p - s : B) : 0;
+        if (nb > 0) or_local_topk(o, K, 0, n, ac, am, ap, labels, price, nb, rc + s, rm + s, rp + s,
+                                  sel ? sel + s : NULL, recs, fc);
+        /* commit(b) */
+        nx[cb] = 0;
+        if (nb == 0) continue;
+        if (s != cursor) { if (stats) stats[2]++; continue; } /* invalidated speculation */
+        done = commit_inherit(o, K, nb, rc + s, rm + s, rp + s, sel ? sel + s : NULL, recs, fc,
+                              X[(b + 2) % 3], b >= 1 ? nx[(b + 2) % 3] : 0, X[cb], &nx[cb],
+                              out_idx + s, out_score + s, out_feas + s);
+        cursor = s + done;
+        if (done < nb) resync = 1;
+        if (stats) { stats[0]++; stats[1] += done < nb; }
+    }
+    /* drain: the last two batches' commits */
+    for (k = 0; k < 3; k++) {
+        int64_t i;
+        int ab = (int)((b - 2 + k + 3) % 3);
+        if (b - 2 + k < 0 || b - 2 + k >= b) continue;
+        for (i = 0; i < nx[ab]; i++) {
+            int32_t j = X[ab][i].idx;
+            ac[j] = X[ab][i].cur[0]; am[j] = X[ab][i].cur[1]; ap[j] = X[ab][i].cur[2];
+        }
+    }
+    for (k = 0; k < 3; k++) free(X[k]);
+    free(recs); free(fc);
+    return OR_OK;
+}

@@ -129,3 +129,33 @@ def test_openmp_oracle_matches_single_thread(oracle_mod):
     a = oracle_mod.schedule(cl, nthreads=1)
     b = oracle_mod.schedule(cl, nthreads=4)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.int64), b[1].view(np.int64))
+
+
+@pytest.mark.parametrize("name,nn,pp,K,B", [("c2", 800, 700, 4, 32), ("c3", 1500, 600, 8, 64),
+                                            ("c5", 2000, 700, 16, 128), ("c3", 700, 500, 4, 128)])
+def test_pipelined_restatement_equals_sequential(oracle_mod, name, nn, pp, K, B):
+    """The GPU pipeline's algorithm (lag-one snapshot, speculative plan, inherited touched set,
+    skip + resync on truncation) equals the sequential semantics."""
+    from ksched import cluster
+    cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    bi, bs, bf, bst, stats = oracle_mod.schedule_pipelined(cl, K, B)
+    assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+    assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+    for a, b in zip(st, bst):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pipelined_restatement_edge_clusters(oracle_mod, seed):
+    from ksched import cluster
+    combos = [(0, 0, False), (0, 1, False), (1, 1, False), (0, 1, True), (1, 1, True), (0, 0, True)]
+    pr, dm, lb = combos[seed]
+    cl = cluster.random_small(91 + seed, n_nodes=96, n_pods=500, priority=pr, domain=dm, use_labels=lb)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    for K, B in ((4, 16), (8, 64), (16, 128)):
+        bi, bs, bf, bst, stats = oracle_mod.schedule_pipelined(cl, K, B)
+        assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+        assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+        for a, b in zip(st, bst):
+            assert np.array_equal(a, b)
