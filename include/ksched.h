@@ -68,7 +68,9 @@ typedef struct ksched_opts {
     int32_t exact_wgs;    /* exact mode: workgroups (0 = auto) */
     int32_t timing;       /* 1: time kernel families with HIP events on the engine stream (sampled) */
     int32_t timing_every; /* batched mode: time one batch in every N (0 = 16) */
-    int32_t reserved[5];
+    int32_t chunk_topk;   /* batched mode: candidates kept per node chunk before the merge, 2/4/8/16 (0 = auto);
+                             capped at topk.  The merge keeps the exact prefix. */
+    int32_t reserved[4];
 } ksched_opts;
 
 typedef struct ksched_ctx ksched_ctx;

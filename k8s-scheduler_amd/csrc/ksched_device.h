@@ -317,4 +317,32 @@ __device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
     return v;
 }
 
+// Wave arg-best via a 64-bit order-preserving max, then (ties only) the lowest node index.
+__device__ __forceinline__ void wave_argbest_fast(double &tk, int32_t &ti, int32_t &ts) {
+    const uint64_t mine = ti == kNoIdx ? 0ull : key_code(tk);
+    const uint64_t best = wave_max_u64(mine);
+    if (best == 0) { tk = -__builtin_inf(); ti = kNoIdx; ts = -1; return; }
+    const uint64_t tie = __ballot(mine == best);
+    int src;
+    if (__popcll(tie) == 1) {
+        src = __ffsll((unsigned long long)tie) - 1;
+    } else {
+        const int32_t mi = wave_min_i32(mine == best ? ti : kNoIdx);
+        src = __ffsll((unsigned long long)__ballot(mine == best && ti == mi)) - 1;
+    }
+    const uint64_t kb = (uint64_t)__double_as_longlong(tk);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(kb >> 32), src);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kb, src);
+    tk = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    ti = __builtin_amdgcn_readlane(ti, src);
+    ts = __builtin_amdgcn_readlane(ts, src);
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int src) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), src);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 }  // namespace ksched

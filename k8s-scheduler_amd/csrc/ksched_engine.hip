@@ -42,7 +42,7 @@ struct ksched_ctx {
     int32_t *d_oidx = nullptr, *d_ofeas = nullptr;
     double *d_osc = nullptr;
     // batched workspace
-    int K = 16, B = 128;
+    int K = 16, KC = 4, B = 128;
     int64_t ws_bytes = 0;
     void *d_ws = nullptr;
     int64_t *d_cursor = nullptr;  // [0] cursor, [1..3] stats
@@ -140,7 +140,7 @@ hipError_t ev_end(ksched_ctx *c, bool on, int fam, int e0, int64_t pairs, hipStr
 
 // Batched-mode geometry for one schedule call.
 struct BatchPlan {
-    int K, B, pod_groups;
+    int K, KC, B, pod_groups;
     int S, n_chunks;       // score kernel: nodes per chunk, chunks
     int stages;            // merge stages (chunk lists -> final)
     int C[4];              // lists per pod entering each stage
@@ -153,6 +153,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 BatchPlan plan_batch(const ksched_ctx *c) {
     BatchPlan pl{};
     pl.K = c->K;
+    pl.KC = c->KC;
     pl.B = c->B;
     pl.pod_groups = (pl.B + 63) / 64;
     const int64_t n = std::max<int64_t>(c->n_local, 1);
@@ -172,7 +173,7 @@ BatchPlan plan_batch(const ksched_ctx *c) {
     }
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    pl.off_part = take((size_t)pl.B * pl.n_chunks * pl.K * sizeof(Cand));
+    pl.off_part = take((size_t)pl.B * pl.n_chunks * pl.KC * sizeof(Cand));
     pl.off_pcnt = take((size_t)pl.B * pl.n_chunks * sizeof(int64_t));
     const int c1 = pl.stages > 1 ? pl.C[1] : 1;
     pl.off_m1 = take((size_t)pl.B * c1 * pl.K * sizeof(Cand) * 2);  // ping-pong for stage >= 1
@@ -233,6 +234,8 @@ int enqueue_batched(ksched_ctx *c) {
     const int poll = env_int("KSCHED_POLL_BATCHES", 0);
     const bool f53 = c->fast53;
     const bool one_stream = env_int("KSCHED_ONE_STREAM", 0) != 0;
+    // lane-per-pod commit for B <= 64 (ksched_commit.hip); the single-wave sequencer otherwise
+    const bool lp_commit = pl.B <= 64 && env_int("KSCHED_LEGACY_COMMIT", 0) == 0;
     hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
@@ -285,7 +288,7 @@ int enqueue_batched(ksched_ctx *c) {
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part);
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt);
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
-            HIPCHK(c, launch_score_topk(pl.K, prio, dom, lab, f53, sa, pl.pod_groups, sS));
+            HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
             const void *in = sa.part;
@@ -293,6 +296,7 @@ int enqueue_batched(ksched_ctx *c) {
             for (int st = 0; st < pl.stages; ++st) {
                 MergeArgs ma{};
                 ma.in = in; ma.in_cnt = in_cnt; ma.C_in = pl.C[st];
+                ma.chunk_input = st == 0 ? 1 : 0;
                 ma.C_out = (pl.C[st] + 63) / 64;
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
@@ -306,7 +310,7 @@ int enqueue_batched(ksched_ctx *c) {
                     ma.out = reinterpret_cast<Cand *>(ws + pl.off_m1) + (size_t)pp * pl.B * c1 * pl.K;
                     ma.out_cnt = reinterpret_cast<int64_t *>(ws + pl.off_m1cnt) + (size_t)pp * pl.B * c1;
                 }
-                HIPCHK(c, launch_merge(pl.K, false, fin, ma, sS));
+                HIPCHK(c, launch_merge(st == 0 ? pl.KC : pl.K, pl.K, false, fin, ma, sS));
                 in = ma.out; in_cnt = ma.out_cnt;
             }
             HIPCHK(c, ev_end(c, tm, 1, e0, 0, sS));
@@ -320,7 +324,7 @@ int enqueue_batched(ksched_ctx *c) {
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists) + (size_t)(b % 2) * pl.B * pl.K;
                 ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc) + (size_t)(b % 2) * pl.B;
-                HIPCHK(c, launch_merge(pl.K, true, true, ma, sS));
+                HIPCHK(c, launch_merge(pl.K, pl.K, true, true, ma, sS));
                 lists = ma.out_rec;
                 fc0 = ma.out_fc;
                 HIPCHK(c, ev_end(c, tm, 3, e0, 0, sS));
@@ -336,7 +340,8 @@ int enqueue_batched(ksched_ctx *c) {
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.dbg = c->d_dbg;
             HIPCHK(c, ev_begin(c, tm, &e0, sC));
-            HIPCHK(c, launch_commit(pl.K, prio, dom, lab, f53, ca, (size_t)lds, sC));
+            if (lp_commit) HIPCHK(c, launch_commit_lp(pl.K, prio, dom, lab, f53, ca, sC));
+            else HIPCHK(c, launch_commit(pl.K, prio, dom, lab, f53, ca, (size_t)lds, sC));
             HIPCHK(c, ev_end(c, tm, 2, e0, 0, sC));
             if (!one_stream) HIPCHK(c, hipEventRecord(c->ev_commit[b % kRing], sC));
         }
@@ -368,6 +373,14 @@ int enqueue_batched(ksched_ctx *c) {
         int64_t hd[16];
         HIPCHK(c, hipStreamSynchronize(sS));
         HIPCHK(c, hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost));
+        if (lp_commit)
+            std::fprintf(stderr, "[ksched commit_lp stamps] pods=%lld kernels=%lld slots=%lld | cycles/kernel: prologue %.0f "
+                         "total %.0f | cycles/pod: reduce %.0f decide %.0f commit+score %.0f advance+out %.0f | skipped %lld | "
+                         "row re-reductions %lld, first touches %lld of %lld placed\n",
+                         (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[7], (double)hd[8] / hd[7],
+                         (double)hd[1] / hd[5], (double)hd[2] / hd[5], (double)hd[3] / hd[5], (double)hd[4] / hd[5],
+                         (long long)h->stats[3], (long long)hd[9], (long long)hd[10], (long long)hd[11]);
+        else
         std::fprintf(stderr, "[ksched commit stamps] pods=%lld kernels=%lld touched=%lld | cycles/pod: loads+rescore %.0f "
                      "reduce %.0f decide %.0f commit+store %.0f | loop cycles/pod %.0f | skipped %lld\n",
                      (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[5], (double)hd[1] / hd[5],
@@ -446,6 +459,9 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     if (!c) return KSCHED_E_NOMEM;
     c->o = *opts;
     c->K = opts->topk ? opts->topk : 16;
+    if (opts->chunk_topk != 0 && opts->chunk_topk != 2 && opts->chunk_topk != 4 && opts->chunk_topk != 8 &&
+        opts->chunk_topk != 16) { delete c; return KSCHED_E_INVALID; }
+    c->KC = std::min(c->K, opts->chunk_topk ? opts->chunk_topk : env_int("KSCHED_CHUNK_TOPK", 4));
     c->B = opts->batch > 0 ? opts->batch : std::min(128, 8 * c->K);
     if (c->B > 128) { delete c; return KSCHED_E_INVALID; }  // touched table: 2B <= 256 = 4 slots per lane
     int ndev = 0;

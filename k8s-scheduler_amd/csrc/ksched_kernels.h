@@ -105,6 +105,7 @@ struct MergeArgs {
     int64_t rank_stride;    // bytes per rank block (INPUT_REC)
     int32_t C_in;
     int32_t C_out;          // ceil(C_in / 64)
+    int32_t chunk_input;    // 1: inputs are score-kernel chunk lists (cut when full)
     Cand *out;              // [B][C_out][K] (non-final)
     int64_t *out_cnt;       // [B][C_out]
     Rec *out_rec;           // [B][K]  (final)
@@ -133,6 +134,8 @@ struct alignas(8) PodStage {
     int64_t rc, rm, rp;
     uint64_t sel;
     int64_t fc0;
+    int32_t cut;  // the pod's merged list is cut (entry 0's pad; see k_merge)
+    int32_t pad;
 };
 constexpr size_t kPodStageBytes = sizeof(PodStage);
 
@@ -158,6 +161,15 @@ constexpr size_t commit_lds_bytes(int B, int K) {
     return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) +
            (size_t)B * (2 * sizeof(Touched) + sizeof(PodStage) + (size_t)K * sizeof(CandStage));
 }
+// Lane-per-pod commit (k_commit_lp, B <= 64): touched slots <= previous batch's commits + this batch's.
+constexpr int kLpSlots = 128;
+constexpr int kLpThreads = 1024;  // prologue: 16 waves re-score the inherited slots; then wave 0 sequences
+constexpr size_t commit_lp_lds_bytes(int K) {
+    return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) + kLpSlots * sizeof(int32_t) +
+           64 * sizeof(int32_t) + kLpSlots * sizeof(Touched) + (size_t)64 * (kLpSlots + 1) * sizeof(double) +
+           (size_t)64 * K * (sizeof(CandStage) + sizeof(double) + sizeof(int32_t));
+}
+static_assert(commit_lp_lds_bytes(16) <= 160 * 1024, "k_commit_lp LDS");
 constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
 
 // host-side launchers (ksched_kernels.hip).  fast53: every allocatable and request magnitude stays
@@ -165,11 +177,12 @@ constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
 hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s);
 hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool fast53, const ExactArgs &a, int block,
                         bool cooperative, hipStream_t s);
-hipError_t launch_score_topk(int K, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
                              hipStream_t s);
-hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
+hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
 hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, size_t lds_bytes,
                          hipStream_t s);
+hipError_t launch_commit_lp(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
 hipError_t launch_plan(Ctl *ctl, int slot, int B, int64_t P, hipStream_t s);
@@ -179,5 +192,30 @@ hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, doub
                                hipStream_t s);
 
 constexpr int kExactBlock = 256;
+
+// (priority, domain, labels, fast53) -> instantiation.  Best-price always ranges over feasible nodes
+// and never divides (fast53 irrelevant).
+#define KSCHED_DISPATCH(prio, dom, lab, f53, CALL)                                              \
+    do {                                                                                        \
+        if ((prio) == kPrioPrice) {                                                             \
+            constexpr int P_ = kPrioPrice, D_ = kDomFeasible; constexpr bool F_ = false;        \
+            if (lab) { constexpr bool L_ = true; return CALL; }                                 \
+            else { constexpr bool L_ = false; return CALL; }                                    \
+        }                                                                                       \
+        constexpr int P_ = kPrioResource;                                                       \
+        if ((dom) == kDomFeasible) {                                                            \
+            constexpr int D_ = kDomFeasible;                                                    \
+            if (lab) { constexpr bool L_ = true;                                                \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+            else { constexpr bool L_ = false;                                                   \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+        } else {                                                                                \
+            constexpr int D_ = kDomAll;                                                         \
+            if (lab) { constexpr bool L_ = true;                                                \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+            else { constexpr bool L_ = false;                                                   \
+                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
+        }                                                                                       \
+    } while (0)
 
 }  // namespace ksched

@@ -195,11 +195,15 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Batched mode, stage 1: fused predicate + score + per-lane top-K.  Lane = pod of the batch, wave =
+// Batched mode, stage 1: fused predicate + score + per-lane top-KC.  Lane = pod of the batch, wave =
 // one node chunk; node rows are wave-uniform (scalar loads of the 96-B NodeRec, reciprocals included).
-// The list is kept sorted by (key desc, idx asc) with a register bubble insert.
+// Chunk c holds the nodes c, c + C, c + 2C, ... (strided): nodes tied on key rank by index, so a
+// strided split spreads the lowest-index ties over all chunks and short chunk lists still merge into a
+// long exact prefix.  A chunk list is "cut" when it holds KC entries (more candidates may exist, all
+// ranking below its last entry); the merge turns that into an exact valid prefix per pod.
+// The list is kept sorted by (key desc, idx asc) with a branch-free register insert.
 // ------------------------------------------------------------------------------------------------
-template <int K, int PRIO, int DOM, bool LAB, bool F53>
+template <int KC, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -217,14 +221,13 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
 
-    double key[K];
-    int32_t idx[K];
+    double key[KC];
+    int32_t idx[KC];
 #pragma unroll
-    for (int q = 0; q < K; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
+    for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
     int64_t cnt = 0;
-    const int64_t j0 = (int64_t)chunk * A.S;
-    const int64_t j1 = (j0 + A.S < A.n_local) ? j0 + A.S : A.n_local;
-    for (int64_t j = j0; j < j1; ++j) {
+    const int64_t C = A.n_chunks;
+    for (int64_t j = chunk; j < A.n_local; j += C) {
         const NodeRec &nd = A.nodes[j];
         const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
         const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
@@ -232,39 +235,41 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
         double k;
         // Nodes arrive in ascending index, so a newcomer loses every tie: a strict key compare keeps
         // the list in (key desc, idx asc) order (empty slots hold -inf and never beat a real key).
-        if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1], nd.af[2],
-                                          nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k) &&
-            k > key[K - 1]) {
-            double ck = k;
-            int32_t ci = (int32_t)(A.node_offset + j);
-            bool moved = false;  // once placed, every later entry shifts down one slot
+        const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1],
+                                                      nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k);
+        double ck = el ? k : -__builtin_inf();
+        int32_t ci = (int32_t)(A.node_offset + j);
+        bool moved = false;  // once placed, every later entry shifts down one slot
 #pragma unroll
-            for (int q = 0; q < K; ++q) {
-                const bool sw = moved || ck > key[q];
-                moved = sw;
-                const double tk = key[q];
-                const int32_t ti = idx[q];
-                key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
-                ck = sw ? tk : ck; ci = sw ? ti : ci;
-            }
+        for (int q = 0; q < KC; ++q) {
+            const bool sw = moved || ck > key[q];
+            moved = sw;
+            const double tk = key[q];
+            const int32_t ti = idx[q];
+            key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+            ck = sw ? tk : ck; ci = sw ? ti : ci;
         }
     }
     if (!active) return;
-    Cand *dst = A.part + ((size_t)b * A.n_chunks + chunk) * K;
+    Cand *dst = A.part + ((size_t)b * A.n_chunks + chunk) * KC;
 #pragma unroll
-    for (int q = 0; q < K; ++q) { dst[q].key = key[q]; dst[q].idx = idx[q]; dst[q].pad = 0; }
+    for (int q = 0; q < KC; ++q) { dst[q].key = key[q]; dst[q].idx = idx[q]; dst[q].pad = 0; }
     A.part_cnt[(size_t)b * A.n_chunks + chunk] = cnt;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Merge: one wave per (pod, group of <= 64 sorted lists).  Each lane stages one list in LDS; K
-// rounds of wave arg-best over the lanes' heads (the winning lane advances).  Final stage writes
+// Merge: one wave per (pod, group of <= 64 sorted lists of KIN entries).  Each lane stages one list in
+// LDS; K rounds of wave arg-best over the lanes' heads (the winning lane advances).  Final stage writes
 // Rec entries carrying the node snapshot state; INPUT_REC merges the ranks' Rec lists.
+// Exact prefix ("cut") rule: a cut input list has unlisted candidates, all ranking below its last
+// entry.  The output keeps only entries ranking at or above the best such cutoff (anything below it
+// could be preceded by an unlisted candidate) and is itself cut when any input was, or when entries
+// were left over after K rounds.  The flag travels in entry 0's pad (Cand) / pad (Rec).
 // ------------------------------------------------------------------------------------------------
-template <int K, bool INPUT_REC, bool FINAL>
+template <int KIN, int K, bool INPUT_REC, bool FINAL>
 __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
-    __shared__ double s_key[64 * K];
-    __shared__ int32_t s_idx[64 * K];
+    __shared__ double s_key[64 * KIN];
+    __shared__ int32_t s_idx[64 * KIN];
     const int lane = threadIdx.x;
     const int grp = blockIdx.x;
     const int b = blockIdx.y;
@@ -273,41 +278,64 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
     const int list = grp * 64 + lane;
     const bool has = list < A.C_in;
     int64_t cnt = 0;
+    int n = 0;          // valid entries of this lane's list
+    bool cut = false;   // this lane's list is cut
     if (has) {
         if (INPUT_REC) {
             const char *blk = static_cast<const char *>(A.in) + (size_t)list * A.rank_stride;
-            const Rec *src = reinterpret_cast<const Rec *>(blk) + (size_t)b * K;
+            const Rec *src = reinterpret_cast<const Rec *>(blk) + (size_t)b * KIN;
 #pragma unroll
-            for (int q = 0; q < K; ++q) {
-                s_key[lane * K + q] = src[q].valid ? src[q].key : -__builtin_inf();
-                s_idx[lane * K + q] = src[q].valid ? src[q].idx : kNoIdx;
+            for (int q = 0; q < KIN; ++q) {
+                const bool v = src[q].valid != 0;
+                s_key[lane * KIN + q] = v ? src[q].key : -__builtin_inf();
+                s_idx[lane * KIN + q] = v ? src[q].idx : kNoIdx;
+                n += v;
             }
-            cnt = reinterpret_cast<const int64_t *>(blk + (size_t)A.B * K * sizeof(Rec))[b];
+            cut = src[0].pad != 0;
+            cnt = reinterpret_cast<const int64_t *>(blk + (size_t)A.B * KIN * sizeof(Rec))[b];
         } else {
-            const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + list) * K;
+            const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + list) * KIN;
 #pragma unroll
-            for (int q = 0; q < K; ++q) { s_key[lane * K + q] = src[q].key; s_idx[lane * K + q] = src[q].idx; }
+            for (int q = 0; q < KIN; ++q) {
+                s_key[lane * KIN + q] = src[q].key;
+                s_idx[lane * KIN + q] = src[q].idx;
+                n += src[q].idx != kNoIdx;
+            }
+            // chunk lists (first stage): cut when full; merged lists carry the flag
+            cut = A.chunk_input ? (n == KIN) : (src[0].pad != 0);
             cnt = A.in_cnt[(size_t)b * A.C_in + list];
         }
     }
     cnt = wave_sum_i64(cnt);
+    // best cutoff over the cut lists (their last valid entry)
+    double ck = (cut && n > 0) ? s_key[lane * KIN + n - 1] : -__builtin_inf();
+    int32_t ci = (cut && n > 0) ? s_idx[lane * KIN + n - 1] : kNoIdx;
+    const bool anycut = __ballot(cut) != 0;
+    {
+        int32_t aux = 0;
+        wave_argbest(ck, ci, aux);
+    }
     __syncthreads();
     int h = 0;
     double mk = -__builtin_inf();
     int32_t mi = kNoIdx, msrc = -1;
     for (int r = 0; r < K; ++r) {
-        double k = (has && h < K) ? s_key[lane * K + h] : -__builtin_inf();
-        int32_t ix = (has && h < K) ? s_idx[lane * K + h] : kNoIdx;
-        int32_t src = lane * K + h;
+        double k = (h < n) ? s_key[lane * KIN + h] : -__builtin_inf();
+        int32_t ix = (h < n) ? s_idx[lane * KIN + h] : kNoIdx;
+        int32_t src = lane * KIN + h;
         wave_argbest(k, ix, src);
         if (ix == kNoIdx) break;  // wave-uniform
-        if (src == lane * K + h) ++h;
+        if (src == lane * KIN + h) ++h;
         if (lane == r) { mk = k; mi = ix; msrc = src; }
     }
+    const bool left = __ballot(h < n) != 0;  // candidates beyond the K output entries
+    // entries ranking below the best cutoff are not exact
+    if (anycut && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
+    const int32_t cut_out = (anycut || left) ? 1 : 0;
     if (!FINAL) {
         if (lane < K) {
             Cand *dst = A.out + ((size_t)b * A.C_out + grp) * K + lane;
-            dst->key = mk; dst->idx = mi; dst->pad = 0;
+            dst->key = mk; dst->idx = mi; dst->pad = lane == 0 ? cut_out : 0;
         }
         if (lane == 0) A.out_cnt[(size_t)b * A.C_out + grp] = cnt;
     } else {
@@ -315,18 +343,19 @@ __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
             Rec r{};
             if (mi != kNoIdx) {
                 if (INPUT_REC) {
-                    const int srcl = msrc / K, srcq = msrc % K;
+                    const int srcl = msrc / KIN, srcq = msrc % KIN;
                     const char *blk = static_cast<const char *>(A.in) + (size_t)(grp * 64 + srcl) * A.rank_stride;
-                    r = reinterpret_cast<const Rec *>(blk)[(size_t)b * K + srcq];
+                    r = reinterpret_cast<const Rec *>(blk)[(size_t)b * KIN + srcq];
                 } else {
                     const NodeRec &nd = A.nodes[mi - A.node_offset];
                     r.key = mk; r.idx = mi; r.valid = 1;
                     r.a[0] = nd.a[0]; r.a[1] = nd.a[1]; r.a[2] = nd.a[2];
-                    r.labels = nd.labels; r.price = nd.price; r.pad = 0;
+                    r.labels = nd.labels; r.price = nd.price;
                 }
             } else {
                 r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
             }
+            r.pad = lane == 0 ? cut_out : 0;
             A.out_rec[(size_t)b * K + lane] = r;
         }
         if (lane == 0) A.out_fc[b] = cnt;
@@ -434,34 +463,6 @@ __device__ __forceinline__ void rescore_touched(const CommitCtx &cx, int64_t rc,
     }
 }
 
-// Wave arg-best via a 64-bit order-preserving max, then (ties only) the lowest node index.
-__device__ __forceinline__ void wave_argbest_fast(double &tk, int32_t &ti, int32_t &ts) {
-    const uint64_t mine = ti == kNoIdx ? 0ull : key_code(tk);
-    const uint64_t best = wave_max_u64(mine);
-    if (best == 0) { tk = -__builtin_inf(); ti = kNoIdx; ts = -1; return; }
-    const uint64_t tie = __ballot(mine == best);
-    int src;
-    if (__popcll(tie) == 1) {
-        src = __ffsll((unsigned long long)tie) - 1;
-    } else {
-        const int32_t mi = wave_min_i32(mine == best ? ti : kNoIdx);
-        src = __ffsll((unsigned long long)__ballot(mine == best && ti == mi)) - 1;
-    }
-    const uint64_t kb = (uint64_t)__double_as_longlong(tk);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(kb >> 32), src);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kb, src);
-    tk = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-    ti = __builtin_amdgcn_readlane(ti, src);
-    ts = __builtin_amdgcn_readlane(ts, src);
-}
-
-__device__ __forceinline__ double readlane_f64(double v, int src) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(b >> 32), src);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
 template <int K, int PRIO, int DOM, bool LAB, bool F53, bool ST>
 __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, int i, const PodStage &ps,
                                             const CandStage &my, uint64_t *ph) {
@@ -478,11 +479,12 @@ __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, 
     const uint64_t umask = __ballot(untouched);
     const int cv = __popcll(vmask);
     const int uq = umask ? __ffsll((unsigned long long)umask) - 1 : K;
-    // threshold a touched node must beat to matter: u*, else list[K-1] (full list), else anything
+    const bool cut = ps.cut != 0;  // unlisted candidates exist, all ranking below the last valid entry
+    // threshold a touched node must beat to matter: u*, else the last valid entry (cut list), else anything
     double thk = -__builtin_inf();
     int32_t thi = kNoIdx;
     if (uq < cv) { thk = readlane_f64(my.key, uq); thi = __builtin_amdgcn_readlane(my.idx, uq); }
-    else if (cv == K) { thk = readlane_f64(my.key, K - 1); thi = __builtin_amdgcn_readlane(my.idx, K - 1); }
+    else if (cut && cv > 0) { thk = readlane_f64(my.key, cv - 1); thi = __builtin_amdgcn_readlane(my.idx, cv - 1); }
     // re-score the nodes already committed (this batch's and the previous batch's)
     int64_t df = 0;
     double tk = -__builtin_inf();
@@ -512,13 +514,15 @@ __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, 
             const int32_t ui = __builtin_amdgcn_readlane(my.idx, uq);
             if (ti != kNoIdx && better(tk, ti, uk, ui)) { kind = 2; wk = tk; wi = ti; }
             else { kind = 1; wk = uk; wi = ui; }
-        } else if (cv < K) {
+        } else if (!cut) {
             if (ti != kNoIdx) { kind = 2; wk = tk; wi = ti; }
-        } else {
-            const double lk = readlane_f64(my.key, K - 1);
-            const int32_t li = __builtin_amdgcn_readlane(my.idx, K - 1);
+        } else if (cv > 0) {
+            const double lk = readlane_f64(my.key, cv - 1);
+            const int32_t li = __builtin_amdgcn_readlane(my.idx, cv - 1);
             if (ti != kNoIdx && better(tk, ti, lk, li)) { kind = 2; wk = tk; wi = ti; }
             else kind = 3;
+        } else {
+            kind = 3;  // unreachable: a cut list keeps at least its cutoff entry
         }
     }
     if (ST) t3 = stamp();
@@ -632,6 +636,8 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
         s.rc = A.pods.rc[p0 + b]; s.rm = A.pods.rm[p0 + b]; s.rp = A.pods.rp[p0 + b];
         s.sel = LAB ? A.pods.sel[p0 + b] : 0;
         s.fc0 = A.fc0[b];
+        s.cut = A.lists[(size_t)b * K].pad;
+        s.pad = 0;
         PS[b] = s;
     }
     for (int e = lane; e < nb * K; e += 64) {
@@ -776,16 +782,17 @@ hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStrea
     }
 }
 
-template <int K, int PRIO, int DOM, bool LAB, bool F53>
+template <int KC, int PRIO, int DOM, bool LAB, bool F53>
 hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
     dim3 grid((a.n_chunks + 3) / 4, pod_groups);
-    hipLaunchKernelGGL((k_score_topk<K, PRIO, DOM, LAB, F53>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 template <int PRIO, int DOM, bool LAB, bool F53>
-hipError_t score_k(int K, const ScoreArgs &a, int pg, hipStream_t s) {
-    switch (K) {
+hipError_t score_k(int KC, const ScoreArgs &a, int pg, hipStream_t s) {
+    switch (KC) {
+        case 2: return score_one<2, PRIO, DOM, LAB, F53>(a, pg, s);
         case 4: return score_one<4, PRIO, DOM, LAB, F53>(a, pg, s);
         case 8: return score_one<8, PRIO, DOM, LAB, F53>(a, pg, s);
         case 16: return score_one<16, PRIO, DOM, LAB, F53>(a, pg, s);
@@ -793,18 +800,30 @@ hipError_t score_k(int K, const ScoreArgs &a, int pg, hipStream_t s) {
     }
 }
 
-template <int K>
-hipError_t merge_k(bool rec, bool fin, const MergeArgs &a, hipStream_t s) {
+template <int KIN, int K>
+hipError_t merge_kk(bool rec, bool fin, const MergeArgs &a, hipStream_t s) {
     dim3 grid(a.C_out, a.B);
     if (rec) {
         if (!fin) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((k_merge<K, true, true>), grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_merge<KIN, K, true, true>), grid, dim3(64), 0, s, a);
     } else if (fin) {
-        hipLaunchKernelGGL((k_merge<K, false, true>), grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_merge<KIN, K, false, true>), grid, dim3(64), 0, s, a);
     } else {
-        hipLaunchKernelGGL((k_merge<K, false, false>), grid, dim3(64), 0, s, a);
+        hipLaunchKernelGGL((k_merge<KIN, K, false, false>), grid, dim3(64), 0, s, a);
     }
     return hipGetLastError();
+}
+
+template <int K>
+hipError_t merge_k(int KIN, bool rec, bool fin, const MergeArgs &a, hipStream_t s) {
+    if (KIN == K) return merge_kk<K, K>(rec, fin, a, s);
+    if (rec) return hipErrorInvalidValue;  // rank lists always hold K entries
+    switch (KIN) {
+        case 2: return merge_kk<2, K>(false, fin, a, s);
+        case 4: return K > 4 ? merge_kk<(K > 4 ? 4 : K), K>(false, fin, a, s) : hipErrorInvalidValue;
+        case 8: return K > 8 ? merge_kk<(K > 8 ? 8 : K), K>(false, fin, a, s) : hipErrorInvalidValue;
+        default: return hipErrorInvalidValue;
+    }
 }
 
 template <int K, int PRIO, int DOM, bool LAB, bool F53>
@@ -830,30 +849,6 @@ hipError_t commit_k(int K, const CommitArgs &a, size_t lds, hipStream_t s) {
     }
 }
 
-// (priority, domain, labels, fast53) -> instantiation.  Best-price always ranges over feasible nodes
-// and never divides (fast53 irrelevant).
-#define KSCHED_DISPATCH(prio, dom, lab, f53, CALL)                                              \
-    do {                                                                                        \
-        if ((prio) == kPrioPrice) {                                                             \
-            constexpr int P_ = kPrioPrice, D_ = kDomFeasible; constexpr bool F_ = false;        \
-            if (lab) { constexpr bool L_ = true; return CALL; }                                 \
-            else { constexpr bool L_ = false; return CALL; }                                    \
-        }                                                                                       \
-        constexpr int P_ = kPrioResource;                                                       \
-        if ((dom) == kDomFeasible) {                                                            \
-            constexpr int D_ = kDomFeasible;                                                    \
-            if (lab) { constexpr bool L_ = true;                                                \
-                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
-            else { constexpr bool L_ = false;                                                   \
-                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
-        } else {                                                                                \
-            constexpr int D_ = kDomAll;                                                         \
-            if (lab) { constexpr bool L_ = true;                                                \
-                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
-            else { constexpr bool L_ = false;                                                   \
-                if (f53) { constexpr bool F_ = true; return CALL; } else { constexpr bool F_ = false; return CALL; } } \
-        }                                                                                       \
-    } while (0)
 
 }  // namespace
 
@@ -868,16 +863,16 @@ hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool f53, const Ex
     KSCHED_DISPATCH(prio, dom, lab, f53, (exact_npt<P_, D_, L_, F_>(npt, a, block, coop, s)));
 }
 
-hipError_t launch_score_topk(int K, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,
                              hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(K, a, pod_groups, s)));
+    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(KC, a, pod_groups, s)));
 }
 
-hipError_t launch_merge(int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s) {
+hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s) {
     switch (K) {
-        case 4: return merge_k<4>(input_rec, final_stage, a, s);
-        case 8: return merge_k<8>(input_rec, final_stage, a, s);
-        case 16: return merge_k<16>(input_rec, final_stage, a, s);
+        case 4: return merge_k<4>(KIN, input_rec, final_stage, a, s);
+        case 8: return merge_k<8>(KIN, input_rec, final_stage, a, s);
+        case 16: return merge_k<16>(KIN, input_rec, final_stage, a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -35,7 +35,8 @@ class Opts(C.Structure):
                 ("domain", C.c_int32), ("use_labels", C.c_int32), ("batch", C.c_int32), ("topk", C.c_int32),
                 ("device", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32),
                 ("node_offset", C.c_int64), ("nodes_global", C.c_int64), ("exact_wgs", C.c_int32),
-                ("timing", C.c_int32), ("timing_every", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("timing", C.c_int32), ("timing_every", C.c_int32), ("chunk_topk", C.c_int32),
+                ("reserved", C.c_int32 * 4)]
 
 
 class Stats(C.Structure):

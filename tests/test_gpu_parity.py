@@ -20,7 +20,10 @@ MODES = None
 def modes():
     from ksched import MODE_BATCHED, MODE_EXACT
     return [("exact", MODE_EXACT, {}), ("batched_k4", MODE_BATCHED, dict(topk=4, batch=32)),
-            ("batched_k8", MODE_BATCHED, dict(topk=8, batch=64)), ("batched_k16", MODE_BATCHED, dict(topk=16, batch=128))]
+            ("batched_k8", MODE_BATCHED, dict(topk=8, batch=64)), ("batched_k16", MODE_BATCHED, dict(topk=16, batch=128)),
+            ("batched_k16_b64", MODE_BATCHED, dict(topk=16, batch=64)),
+            ("batched_k16_b64_c2", MODE_BATCHED, dict(topk=16, batch=64, chunk_topk=2)),
+            ("batched_k8_b128_c8", MODE_BATCHED, dict(topk=8, batch=128, chunk_topk=8))]
 
 
 def run_engine(cl, mode, **kw):
@@ -51,7 +54,7 @@ def golden():
         return json.load(f)
 
 
-@pytest.mark.parametrize("mi", range(4), ids=["exact", "b4", "b8", "b16"])
+@pytest.mark.parametrize("mi", range(7), ids=["exact", "b4", "b8", "b16", "b16_64", "b16_64_c2", "b8_128_c8"])
 def test_golden_clusters(gpu_available, mi):
     from test_oracle import _cluster_from
     name, mode, kw = modes()[mi]
@@ -89,6 +92,20 @@ def test_config_prefix_parity(gpu_available, oracle_mod, name, nn, pp):
     want = oracle_mod.schedule(cl, nthreads=8)
     for mname, mode, kw in modes():
         assert_same(run_engine(cl, mode, **kw), want, f"{name}/{mname}")
+
+
+@pytest.mark.parametrize("kc", [2, 4, 16])
+def test_tie_storm_chunk_cut(gpu_available, oracle_mod, kc):
+    """Identical nodes and identical pods: every key ties and ranks by node index, so the merged list's
+    exact prefix depends entirely on the strided chunking + cut rule; zero-request pods mixed in."""
+    from ksched import MODE_BATCHED, cluster
+    n, p = 3000, 900
+    cl = cluster.Cluster(name="ties", alloc_cpu=np.full(n, 4000, np.int64), alloc_mem=np.full(n, 8388608, np.int64),
+                         alloc_pods=np.full(n, 110, np.int64), req_cpu=np.where(np.arange(p) % 3 == 0, 0, 200).astype(np.int64),
+                         req_mem=np.where(np.arange(p) % 3 == 0, 0, 65536).astype(np.int64), req_pods=np.ones(p, np.int64))
+    want = oracle_mod.schedule(cl)
+    for b in (64, 128):
+        assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=b, chunk_topk=kc), want, f"ties kc={kc} b={b}")
 
 
 def test_exact_mode_workgroup_counts(gpu_available, oracle_mod):
@@ -157,8 +174,9 @@ def test_full_size_c3_batched_equals_exact(gpu_available):
     from ksched import MODE_BATCHED, MODE_EXACT, cluster
     cl = cluster.make_cluster("c3")
     a = run_engine(cl, MODE_EXACT)
-    b = run_engine(cl, MODE_BATCHED, topk=16, batch=128)
-    assert_same(b, a[:4], "c3 full exact-vs-batched")
+    for kw in (dict(topk=16, batch=128), dict(topk=16, batch=64), dict(topk=8, batch=32)):
+        b = run_engine(cl, MODE_BATCHED, **kw)
+        assert_same(b, a[:4], f"c3 full exact-vs-batched {kw}")
     oi = a[0]
     placed = oi >= 0
     exp_c = cl.alloc_cpu.copy(); exp_m = cl.alloc_mem.copy(); exp_p = cl.alloc_pods.copy()
