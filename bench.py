@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--topk", type=int, default=16)
-    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-baseline-s", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify a prefix against the CPU oracle")

@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
         if (tid == 0) {
             A.xout->count = 0;
             if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
+            plan_after_commit(A, false, cursor);
         }
         return;
     }
@@ -356,10 +357,10 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
     if (lane == 0) {
         A.xout->count = base;
         A.ctl->cursor = p0 + done;
-        if (done < nb) A.ctl->resync = 1;
         A.ctl->stats[0] += 1;
         A.ctl->stats[1] += (done < nb) ? 1 : 0;
         A.ctl->stats[2] += placed;
+        plan_after_commit(A, done < nb, p0 + done);
         if (ST) {
             A.dbg[0] += ph[0]; A.dbg[1] += ph[1]; A.dbg[2] += ph[2]; A.dbg[3] += ph[3]; A.dbg[4] += ph[4];
             A.dbg[5] += done; A.dbg[6] += nT; A.dbg[7] += 1; A.dbg[8] += lp_stamp() - tp0;

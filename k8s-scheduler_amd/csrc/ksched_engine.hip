@@ -208,12 +208,13 @@ int decide_fast53(ksched_ctx *c) {
 }
 
 // Batched mode, software-pipelined over two streams:
-//   stream S: [wait commit(b-2)] apply(b-2) -> plan(b) -> score(b) -> merge(b) [-> all-gather -> rank merge]
-//   stream C: [wait lists(b)]    commit(b)
+//   stream S: [wait commit(b-2)] score(b) (+ overlay/write-back of b-2's commits) -> merge(b)
+//             [-> all-gather -> rank merge]
+//   stream C: [wait lists(b)]    commit(b) (+ plan of batch b+2)
 // score(b) runs on every CU while commit(b-1) runs on one; commit(b) inherits the nodes committed by
-// batch b-1 (its score snapshot is one batch older) and node rows are written by apply only after
-// the next score has read them.  Each batch's start is planned speculatively (previous start + B);
-// a truncated batch invalidates the in-flight speculation, which commit skips and plan resyncs.
+// batch b-1 (its score snapshot is one batch older).  Each batch's start is planned speculatively
+// (previous start + B) by the commit two batches back; a truncated batch invalidates the in-flight
+// speculation, which commit skips, and plans its restart at the committed frontier.
 int enqueue_batched(ksched_ctx *c) {
     const BatchPlan pl = plan_batch(c);
     if (c->ws_bytes < (int64_t)pl.total) {
@@ -256,7 +257,7 @@ int enqueue_batched(ksched_ctx *c) {
         return reinterpret_cast<XBuf *>(static_cast<char *>(c->d_xring) + (size_t)slot * xb);
     };
     Ctl *ctl = reinterpret_cast<Ctl *>(c->d_cursor);
-    HIPCHK(c, hipMemsetAsync(ctl, 0, sizeof(Ctl), sS));
+    HIPCHK(c, launch_ctl_init(ctl, pl.B, c->p, sS));
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
     if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
@@ -276,17 +277,15 @@ int enqueue_batched(ksched_ctx *c) {
             const int slot = (int)(b % kPlanRing);
             const int64_t *plan = &ctl->plan[slot];
             char *lists_base = static_cast<char *>(c->d_lring) + (size_t)(b % kRing) * pl.send_bytes;
-            // S: write back batch b-2's commits (score(b-1) has read the old rows), then plan + score b
-            if (b >= 2) {
-                if (!one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[(b - 2) % kRing], 0));
-                HIPCHK(c, launch_apply_batch(xbuf(b - 2), c->d_nodes, c->o.node_offset, c->n_local, sS));
-            }
-            HIPCHK(c, launch_plan(ctl, slot, pl.B, c->p, sS));
+            // S: score b once commit(b-2) is done (its plan for b and its committed nodes, which score(b)
+            // overlays on the rows it reads and writes back)
+            if (b >= 2 && !one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[(b - 2) % kRing], 0));
             ScoreArgs sa{};
             sa.nodes = c->d_nodes; sa.n_local = c->n_local; sa.node_offset = c->o.node_offset;
             sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = plan; sa.B = pl.B;
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part);
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt);
+            sa.patch = xbuf(b - 2);
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
             HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
@@ -336,6 +335,8 @@ int enqueue_batched(ksched_ctx *c) {
             // C: ordered commit of batch b
             CommitArgs ca{};
             ca.lists = lists; ca.fc0 = fc0; ca.pods = pods; ca.plan = plan; ca.ctl = ctl; ca.B = pl.B;
+            ca.plan1 = &ctl->plan[(b + 1) % kPlanRing];
+            ca.plan2 = &ctl->plan[(b + 2) % kPlanRing];
             ca.xin = xbuf(b - 1); ca.xout = xbuf(b);
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.dbg = c->d_dbg;

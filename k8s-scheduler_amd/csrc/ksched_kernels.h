@@ -86,7 +86,7 @@ struct ExactArgs {
 };
 
 struct ScoreArgs {
-    const NodeRec *nodes;
+    NodeRec *nodes;    // read; the rows of `patch` are written back by their chunk's wave
     int64_t n_local;
     int64_t node_offset;
     int32_t S;         // nodes per chunk (one wave per chunk and 64 pods)
@@ -94,8 +94,9 @@ struct ScoreArgs {
     PodArgs pods;
     const int64_t *cursor;  // this batch's plan slot (first pod, or -1)
     int32_t B;
-    Cand *part;        // [B][n_chunks][K]
+    Cand *part;        // [B][n_chunks][KC]
     int64_t *part_cnt; // [B][n_chunks]
+    const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
 };
 
 struct MergeArgs {
@@ -122,6 +123,8 @@ struct CommitArgs {
     const int64_t *fc0;     // [B]
     PodArgs pods;
     const int64_t *plan;    // this batch's plan slot
+    const int64_t *plan1;   // the next batch's plan slot (already set)
+    int64_t *plan2;         // the slot of the batch after next: written by this commit
     Ctl *ctl;
     int32_t B;
     const XBuf *xin;        // nodes committed by the previous batch (relative to this batch's snapshot)
@@ -161,6 +164,16 @@ constexpr size_t commit_lds_bytes(int B, int K) {
     return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) +
            (size_t)B * (2 * sizeof(Touched) + sizeof(PodStage) + (size_t)K * sizeof(CandStage));
 }
+// Speculative planning, done by the commit of batch k for batch k+2 (stream order makes plan(k+2)
+// visible to score(k+2), which waits for commit(k)): after a truncation restart at the committed
+// frontier, otherwise continue one batch after plan(k+1).  -1 = past the last pod.
+__device__ __forceinline__ void plan_after_commit(const CommitArgs &A, bool truncated, int64_t cursor) {
+    const int64_t n1 = *A.plan1;
+    int64_t nx = truncated ? cursor : (n1 < 0 ? -1 : n1 + A.B);
+    if (nx >= A.pods.p) nx = -1;
+    *A.plan2 = nx;
+}
+
 // Lane-per-pod commit (k_commit_lp, B <= 64): touched slots <= previous batch's commits + this batch's.
 constexpr int kLpSlots = 128;
 constexpr int kLpThreads = 1024;  // prologue: 16 waves re-score the inherited slots; then wave 0 sequences
@@ -185,7 +198,7 @@ hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const 
 hipError_t launch_commit_lp(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
-hipError_t launch_plan(Ctl *ctl, int slot, int B, int64_t P, hipStream_t s);
+hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s);
 hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s);
 // diagnostics: qdiv(a, b, recip(b)) against the native a / b, bit for bit
 hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,

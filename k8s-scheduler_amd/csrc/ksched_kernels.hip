@@ -209,6 +209,27 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int chunk = blockIdx.x * 4 + wave;
     if (chunk >= A.n_chunks) return;
+    const int64_t C = A.n_chunks;
+    // Batch b-2's commits (<= 128 nodes, two per lane): this wave owns the ones in its chunk.  It
+    // writes them back to the rows (for the next launches) and overlays them on what it reads in this
+    // launch, so no separate apply kernel has to run between commit(b-2) and score(b).
+    int64_t pj0 = -1, pj1 = -1;  // local node index of entries lane and lane + 64, if in this chunk
+    {
+        const int np = A.patch->count;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int e = h * 64 + lane;
+            const int64_t j = e < np ? (int64_t)A.patch->e[e].idx - A.node_offset : -1;
+            const bool mine = j >= 0 && j < A.n_local && (j % C) == chunk;
+            if (mine && blockIdx.y == 0) {
+                const XRec &x = A.patch->e[e];
+                set_node(A.nodes + j, x.cur[0], x.cur[1], x.cur[2]);
+            }
+            if (h == 0) pj0 = mine ? j : -1;
+            else pj1 = mine ? j : -1;
+        }
+    }
+    const bool anyp = __ballot(pj0 >= 0 || pj1 >= 0) != 0;
     const int64_t p0 = *A.cursor;
     if (p0 < 0 || p0 >= A.pods.p) return;
     const int b = blockIdx.y * 64 + lane;
@@ -226,17 +247,28 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
 #pragma unroll
     for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
     int64_t cnt = 0;
-    const int64_t C = A.n_chunks;
     for (int64_t j = chunk; j < A.n_local; j += C) {
         const NodeRec &nd = A.nodes[j];
-        const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+        int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+        double af0 = nd.af[0], af1 = nd.af[1], af2 = nd.af[2], y0 = nd.y[0], y1 = nd.y[1], y2 = nd.y[2];
+        if (anyp) {  // wave-uniform: this chunk holds committed nodes of batch b-2
+            const uint64_t hit = __ballot(pj0 == j || pj1 == j);
+            if (hit) {
+                const int src = __ffsll((unsigned long long)hit) - 1;
+                const int e = __builtin_amdgcn_readlane(pj0 == j ? lane : lane + 64, src);
+                const XRec &xr = A.patch->e[e];
+                ac = xr.cur[0]; am = xr.cur[1]; ap = xr.cur[2];
+                af0 = (double)ac; af1 = (double)am; af2 = (double)ap;
+                y0 = recip_or_zero(ac, af0); y1 = recip_or_zero(am, af1); y2 = recip_or_zero(ap, af2);
+            }
+        }
         const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
         cnt += f;
         double k;
         // Nodes arrive in ascending index, so a newcomer loses every tie: a strict key compare keeps
         // the list in (key desc, idx asc) order (empty slots hold -inf and never beat a real key).
-        const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1],
-                                                      nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k);
+        const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, af0, af1, af2, y0, y1,
+                                                      y2, y3, nd.price, &k);
         double ck = el ? k : -__builtin_inf();
         int32_t ci = (int32_t)(A.node_offset + j);
         bool moved = false;  // once placed, every later entry shifts down one slot
@@ -609,6 +641,7 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
         if (lane == 0) {
             A.xout->count = 0;
             if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
+            plan_after_commit(A, false, cursor);
         }
         return;
     }
@@ -702,26 +735,22 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
     if (lane == 0) {
         A.xout->count = base;
         A.ctl->cursor = p0 + done;
-        if (done < nb) A.ctl->resync = 1;
         A.ctl->stats[0] += 1;
         A.ctl->stats[1] += (done < nb) ? 1 : 0;
         A.ctl->stats[2] += cx.placed;
+        plan_after_commit(A, done < nb, p0 + done);
     }
 }
 
-// Plan the next speculative batch: restart at the committed frontier after a truncation, else
-// continue one full batch after the previous plan.
-__global__ void k_plan(Ctl *ctl, int slot, int B, int64_t P) {
+// Pipeline control at the start of a batched call: batch 0 starts at pod 0, batch 1 speculatively at B;
+// every later plan is written by the commit two batches earlier (plan_after_commit).
+__global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     if (threadIdx.x != 0) return;
-    int64_t start;
-    if (ctl->resync) {
-        start = ctl->cursor;
-        ctl->resync = 0;
-    } else {
-        start = ctl->spec_next;
-    }
-    ctl->spec_next = start + B;
-    ctl->plan[slot] = start < P ? start : -1;
+    ctl->cursor = 0; ctl->spec_next = 0; ctl->resync = 0;
+    for (int i = 0; i < 5; ++i) ctl->stats[i] = 0;
+    for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;
+    ctl->plan[0] = P > 0 ? 0 : -1;
+    ctl->plan[1] = B < P ? B : -1;
 }
 
 // Write one batch's committed nodes into this rank's node rows.
@@ -888,8 +917,8 @@ hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_
     return hipGetLastError();
 }
 
-hipError_t launch_plan(Ctl *ctl, int slot, int B, int64_t P, hipStream_t s) {
-    hipLaunchKernelGGL(k_plan, dim3(1), dim3(64), 0, s, ctl, slot, B, P);
+hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, s, ctl, B, P);
     return hipGetLastError();
 }
 
