@@ -48,6 +48,11 @@ extern "C" {
 #define KSCHED_PRIORITY_RESOURCE 0    /* (balanced + least-requested) / 2, anchor/priorities.go:45-50 */
 #define KSCHED_PRIORITY_BEST_PRICE 1  /* lowest node price among feasible nodes (README.md:37-64; build-defined) */
 
+/* ordered-commit implementations (batched mode; all produce the sequential result) */
+#define KSCHED_COMMIT_SEQUENTIAL 1    /* one wave re-scores the touched set per pod (batch <= 128) */
+#define KSCHED_COMMIT_LANE_PER_POD 2  /* one wave, lane = pod, incremental pod x touched-node keys (batch <= 64) */
+#define KSCHED_COMMIT_SPECULATIVE 3   /* guess first touches, check all pods in parallel, resolve the first miss (batch <= 64) */
+
 #define KSCHED_DOMAIN_ALL 0       /* argmax over ALL nodes, feasible or not (the reference, anchor/priorities.go:45) */
 #define KSCHED_DOMAIN_FEASIBLE 1  /* argmax over feasible nodes only (build extension) */
 
@@ -70,7 +75,8 @@ typedef struct ksched_opts {
     int32_t timing_every; /* batched mode: time one batch in every N (0 = 16) */
     int32_t chunk_topk;   /* batched mode: candidates kept per node chunk before the merge, 2/4/8/16 (0 = auto);
                              capped at topk.  The merge keeps the exact prefix. */
-    int32_t reserved[4];
+    int32_t commit_impl;  /* batched mode: KSCHED_COMMIT_* (0 = auto: speculative when batch <= 64) */
+    int32_t reserved[3];
 } ksched_opts;
 
 typedef struct ksched_ctx ksched_ctx;

@@ -31,6 +31,7 @@ struct LpSmem {
     uint32_t *filt;   // 64K-bit filter in front of the hash
     int32_t *ti;      // node index per touched slot
     int32_t *dfacc;   // per pod: sum over inherited slots of fits(cur) - fits(s0)
+    uint32_t *tm;     // per pod: bit q = list entry q's node is inherited (in T at the start)
     Touched *T;       // touched slots
     double *S;        // [64 pods][kLpRow] key of (pod, slot); -inf = not eligible
     CandStage *CS;    // [64 pods][K] staged candidate lists (node snapshot state; wave-uniform reads)
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
     m.filt = reinterpret_cast<uint32_t *>(p); p += kTouchFilterWords * sizeof(uint32_t);
     m.ti = reinterpret_cast<int32_t *>(p); p += kLpSlots * sizeof(int32_t);
     m.dfacc = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+    m.tm = reinterpret_cast<uint32_t *>(p); p += 64 * sizeof(uint32_t);
     m.T = reinterpret_cast<Touched *>(p); p += kLpSlots * sizeof(Touched);
     m.S = reinterpret_cast<double *>(p); p += (size_t)64 * kLpRow * sizeof(double);
     m.CS = reinterpret_cast<CandStage *>(p); p += (size_t)64 * K * sizeof(CandStage);
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
     // ---- prologue (all waves): stage lists, inherit the previous batch's commits ----
     for (int w = tid; w < kTouchHash; w += kLpThreads) m.hkey[w] = -1;
     for (int w = tid; w < kTouchFilterWords; w += kLpThreads) m.filt[w] = 0;
-    if (tid < 64) m.dfacc[tid] = 0;
+    if (tid < 64) { m.dfacc[tid] = 0; m.tm[tid] = 0; }
     for (int e = tid; e < nb * K; e += kLpThreads) {
         const Rec r = A.lists[e];
         CandStage c;
@@ -150,9 +152,13 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
     const double y3 = recip(3.0);
     double *Srow = m.S + (size_t)lane * kLpRow;
 
-    // inherited slots: every pod's key against the slot's current state, and its predicate delta
+    // inherited slots (all waves): every pod's key against the slot's current state, its predicate
+    // delta and a per-wave partial row best; list entry q's touched bit by wave q.  Columns 64..95 of
+    // S are free during the prologue (inherited slots < 64) and hold the partial row bests.
     {
         int dfl = 0;
+        double pk = -__builtin_inf();
+        int32_t pi = kNoIdx, ps = -1;
         for (int t = wave; t < nin; t += nw) {
             const Touched &x = m.T[t];
             const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
@@ -162,9 +168,22 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
             const bool el = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
                                                           x.curf[0], x.curf[1], x.curf[2], x.cury[0], x.cury[1],
                                                           x.cury[2], y3, x.price, &k);
-            Srow[t] = el ? k : -__builtin_inf();
+            k = el ? k : -__builtin_inf();
+            Srow[t] = k;
+            const bool up = el && better(k, m.ti[t], pk, pi);
+            pk = up ? k : pk;
+            pi = up ? m.ti[t] : pi;
+            ps = up ? t : ps;
+        }
+        if (wave < nin) {
+            Srow[64 + wave] = pk;
+            reinterpret_cast<int64_t *>(Srow)[80 + wave] = ((int64_t)ps << 32) | (uint32_t)pi;
         }
         if (dfl != 0) atomicAdd(&m.dfacc[lane], dfl);
+        if (nin > 0 && wave < K && pj) {
+            const int32_t x = m.LI[wave * 64 + lane];
+            if (x != kNoIdx && lp_has(m, x)) atomicOr(&m.tm[lane], 1u << wave);
+        }
     }
     __syncthreads();
     if (wave != 0) return;
@@ -175,7 +194,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
     // best of row j of S (rbk, rbi, rbs).  A commit only ever changes one column of S, so the running
     // best stays exact unless the column holding it got worse ("dirty"); only then is row i
     // re-reduced across the wave when pod i's turn comes.
-    int64_t fc = pj ? A.fc0[lane] + m.dfacc[lane] : 0;
+    int32_t fc = pj ? (int32_t)(A.fc0[lane] + m.dfacc[lane]) : 0;  // <= nodes < 2^31
     const int cut = pj ? A.lists[(size_t)lane * K].pad : 0;  // unlisted candidates rank below the last entry
     const double *LKl = m.LK + lane;  // entry q of this lane's list at [q * 64]
     const int32_t *LIl = m.LI + lane;
@@ -187,23 +206,25 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
         cv += li[q] != kNoIdx;  // valid entries form a prefix
     }
     const uint32_t vmask = (1u << cv) - 1u;  // cv <= 16
-    uint32_t tmask = 0;
-    if (nin > 0) {
-#pragma unroll
-        for (int q = 0; q < K; ++q)
-            if (q < cv && lp_has(m, li[q])) tmask |= 1u << q;
-    }
+    uint32_t tmask = m.tm[lane];
     int ptr = __builtin_ctz((~tmask & vmask) | (1u << cv));
     double uk = ptr < cv ? LKl[ptr * 64] : -__builtin_inf();
     int32_t ui = ptr < cv ? LIl[ptr * 64] : kNoIdx;
     double rbk = -__builtin_inf();
     int32_t rbi = kNoIdx, rbs = -1;
     bool dirty = false;
-    for (int t = 0; t < nin; ++t) {
-        const double k = Srow[t];
-        const int32_t x = m.ti[t];
-        if (k != -__builtin_inf() && better(k, x, rbk, rbi)) { rbk = k; rbi = x; rbs = t; }
+    {
+        const int nwp = nin < nw ? nin : nw;
+        for (int w = 0; w < nwp; ++w) {
+            const double k = Srow[64 + w];
+            const int64_t pk = reinterpret_cast<const int64_t *>(Srow)[80 + w];
+            const int32_t x = (int32_t)(uint32_t)pk;
+            if (k != -__builtin_inf() && better(k, x, rbk, rbi)) { rbk = k; rbi = x; rbs = (int32_t)(pk >> 32); }
+        }
     }
+    // this lane's pod outcome, captured at its turn and stored once at the end
+    int32_t my_idx = 0, my_feas = 0;
+    double my_score = 0.0;
 
     int nT = nin;
     int64_t placed = 0, nred = 0, nk1 = 0;
@@ -238,7 +259,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
         ti = __builtin_amdgcn_readfirstlane(ti);
         ts = __builtin_amdgcn_readfirstlane(ts);
         if (ST) { tb = lp_stamp(); ph[1] += tb - ta; ta = tb; }
-        const int64_t fci = readlane_i64(fc, i);
+        const int32_t fci = __builtin_amdgcn_readlane(fc, i);
         const int pi = __builtin_amdgcn_readlane(ptr, i);
         const int cvi = __builtin_amdgcn_readlane(cv, i);
         const int cuti = __builtin_amdgcn_readlane(cut, i);
@@ -292,7 +313,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
             // every pod's view of node wi: predicate delta and exact key at the new state
             const bool fo = fits(rc, rm, rp, sel, b0, b1, b2, lab, LAB);
             const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
-            fc += (int64_t)fn - (int64_t)fo;
+            fc += (int32_t)fn - (int32_t)fo;
             double k;
             const bool el = pair_key_fast<PRIO, DOM, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, nf0, nf1, nf2, ny0,
                                                           ny1, ny2, y3, pr, &k);
@@ -327,17 +348,17 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
                 }
             }
         }
-        if (lane == 0) {
-            const int64_t pod = p0 + i;
-            A.out.idx[pod] = oidx;
-            A.out.score[pod] = osc;
-            A.out.feas[pod] = (int32_t)fci;
-        }
+        if (lane == i) { my_idx = oidx; my_score = osc; my_feas = fci; }
         if (ST) { tb = lp_stamp(); ph[4] += tb - ta; ta = tb; }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < done) {
+        A.out.idx[p0 + lane] = my_idx;
+        A.out.score[p0 + lane] = my_score;
+        A.out.feas[p0 + lane] = my_feas;
+    }
     // export this batch's commits (wave-ordered compaction)
     int base = 0;
     for (int t0 = 0; t0 < nT; t0 += 64) {

@@ -235,8 +235,13 @@ int enqueue_batched(ksched_ctx *c) {
     const int poll = env_int("KSCHED_POLL_BATCHES", 0);
     const bool f53 = c->fast53;
     const bool one_stream = env_int("KSCHED_ONE_STREAM", 0) != 0;
-    // lane-per-pod commit for B <= 64 (ksched_commit.hip); the single-wave sequencer otherwise
-    const bool lp_commit = pl.B <= 64 && env_int("KSCHED_LEGACY_COMMIT", 0) == 0;
+    // commit implementation: speculative-parallel (B <= 64, default), lane-per-pod (B <= 64), or the
+    // single-wave sequencer (any B <= 128)
+    int impl = c->o.commit_impl ? c->o.commit_impl : env_int("KSCHED_COMMIT_IMPL", 0);
+    if (impl == 0) impl = pl.B <= 64 ? KSCHED_COMMIT_SPECULATIVE : KSCHED_COMMIT_SEQUENTIAL;
+    if (impl != KSCHED_COMMIT_SEQUENTIAL && pl.B > 64) impl = KSCHED_COMMIT_SEQUENTIAL;
+    const bool lp_commit = impl == KSCHED_COMMIT_LANE_PER_POD;
+    const bool spc_commit = impl == KSCHED_COMMIT_SPECULATIVE;
     hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
@@ -341,7 +346,8 @@ int enqueue_batched(ksched_ctx *c) {
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.dbg = c->d_dbg;
             HIPCHK(c, ev_begin(c, tm, &e0, sC));
-            if (lp_commit) HIPCHK(c, launch_commit_lp(pl.K, prio, dom, lab, f53, ca, sC));
+            if (spc_commit) HIPCHK(c, launch_commit_spc(pl.K, prio, dom, lab, f53, ca, sC));
+            else if (lp_commit) HIPCHK(c, launch_commit_lp(pl.K, prio, dom, lab, f53, ca, sC));
             else HIPCHK(c, launch_commit(pl.K, prio, dom, lab, f53, ca, (size_t)lds, sC));
             HIPCHK(c, ev_end(c, tm, 2, e0, 0, sC));
             if (!one_stream) HIPCHK(c, hipEventRecord(c->ev_commit[b % kRing], sC));
@@ -374,7 +380,13 @@ int enqueue_batched(ksched_ctx *c) {
         int64_t hd[16];
         HIPCHK(c, hipStreamSynchronize(sS));
         HIPCHK(c, hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost));
-        if (lp_commit)
+        if (spc_commit)
+            std::fprintf(stderr, "[ksched commit_spc] kernels=%lld rounds=%lld failures=%lld (%.3f rounds/batch) | "
+                         "cycles/kernel: prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
+                         (long long)hd[14], (long long)hd[12], (long long)hd[13], (double)hd[12] / (hd[14] ? hd[14] : 1),
+                         (double)hd[0] / hd[14], (double)hd[1] / hd[14], (double)hd[2] / hd[14], (double)hd[3] / hd[14],
+                         (double)hd[4] / hd[14]);
+        else if (lp_commit)
             std::fprintf(stderr, "[ksched commit_lp stamps] pods=%lld kernels=%lld slots=%lld | cycles/kernel: prologue %.0f "
                          "total %.0f | cycles/pod: reduce %.0f decide %.0f commit+score %.0f advance+out %.0f | skipped %lld | "
                          "row re-reductions %lld, first touches %lld of %lld placed\n",
@@ -464,7 +476,8 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
         opts->chunk_topk != 16) { delete c; return KSCHED_E_INVALID; }
     c->KC = std::min(c->K, opts->chunk_topk ? opts->chunk_topk : env_int("KSCHED_CHUNK_TOPK", 4));
     c->B = opts->batch > 0 ? opts->batch : std::min(128, 8 * c->K);
-    if (c->B > 128) { delete c; return KSCHED_E_INVALID; }  // touched table: 2B <= 256 = 4 slots per lane
+    if (c->B > 128) { delete c; return KSCHED_E_INVALID; }
+    if (opts->commit_impl < 0 || opts->commit_impl > 3) { delete c; return KSCHED_E_INVALID; }  // touched table: 2B <= 256 = 4 slots per lane
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { delete c; return KSCHED_E_DEVICE; }
     if (opts->device >= 0) {

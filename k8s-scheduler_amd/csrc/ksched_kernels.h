@@ -179,7 +179,7 @@ constexpr int kLpSlots = 128;
 constexpr int kLpThreads = 1024;  // prologue: 16 waves re-score the inherited slots; then wave 0 sequences
 constexpr size_t commit_lp_lds_bytes(int K) {
     return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) + kLpSlots * sizeof(int32_t) +
-           64 * sizeof(int32_t) + kLpSlots * sizeof(Touched) + (size_t)64 * (kLpSlots + 1) * sizeof(double) +
+           2 * 64 * sizeof(int32_t) + kLpSlots * sizeof(Touched) + (size_t)64 * (kLpSlots + 1) * sizeof(double) +
            (size_t)64 * K * (sizeof(CandStage) + sizeof(double) + sizeof(int32_t));
 }
 static_assert(commit_lp_lds_bytes(16) <= 160 * 1024, "k_commit_lp LDS");
@@ -195,6 +195,8 @@ hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, c
 hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
 hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, size_t lds_bytes,
                          hipStream_t s);
+constexpr int kSpcThreads = 512;  // speculative commit: wave 0 guesses and checks, 8 waves evaluate
+hipError_t launch_commit_spc(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
 hipError_t launch_commit_lp(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);

@@ -36,7 +36,7 @@ class Opts(C.Structure):
                 ("device", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32),
                 ("node_offset", C.c_int64), ("nodes_global", C.c_int64), ("exact_wgs", C.c_int32),
                 ("timing", C.c_int32), ("timing_every", C.c_int32), ("chunk_topk", C.c_int32),
-                ("reserved", C.c_int32 * 4)]
+                ("commit_impl", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class Stats(C.Structure):

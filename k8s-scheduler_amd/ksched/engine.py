@@ -26,7 +26,8 @@ class Engine:
     def __init__(self, mode: int = L.MODE_AUTO, priority: int = L.PRIORITY_RESOURCE, domain: int = L.DOMAIN_ALL,
                  use_labels: bool = False, batch: int = 0, topk: int = 0, device: int = -1,
                  rank: int = 0, nranks: int = 1, node_offset: int = 0, nodes_global: int = 0, exact_wgs: int = 0,
-                 timing: bool = False, timing_every: int = 0, chunk_topk: int = 0):
+                 timing: bool = False, timing_every: int = 0, chunk_topk: int = 0,
+                 commit_impl: int = 0):
         lb = L.lib()
         o = L.Opts()
         L.check(lb.ksched_default_opts(C.byref(o)), what="default_opts")
@@ -34,6 +35,7 @@ class Engine:
         o.batch, o.topk, o.device = batch, topk, device
         o.rank, o.nranks, o.node_offset, o.nodes_global, o.exact_wgs = rank, nranks, node_offset, nodes_global, exact_wgs
         o.timing, o.timing_every, o.chunk_topk = int(bool(timing)), timing_every, chunk_topk
+        o.commit_impl = commit_impl
         ctx = L.CTX()
         L.check(lb.ksched_create(C.byref(o), C.byref(ctx)), what="create")
         self._ctx = ctx

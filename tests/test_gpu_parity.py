@@ -23,7 +23,9 @@ def modes():
             ("batched_k8", MODE_BATCHED, dict(topk=8, batch=64)), ("batched_k16", MODE_BATCHED, dict(topk=16, batch=128)),
             ("batched_k16_b64", MODE_BATCHED, dict(topk=16, batch=64)),
             ("batched_k16_b64_c2", MODE_BATCHED, dict(topk=16, batch=64, chunk_topk=2)),
-            ("batched_k8_b128_c8", MODE_BATCHED, dict(topk=8, batch=128, chunk_topk=8))]
+            ("batched_k8_b128_c8", MODE_BATCHED, dict(topk=8, batch=128, chunk_topk=8)),
+            ("batched_k16_b64_lp", MODE_BATCHED, dict(topk=16, batch=64, commit_impl=2)),
+            ("batched_k8_b48_seq", MODE_BATCHED, dict(topk=8, batch=48, commit_impl=1))]
 
 
 def run_engine(cl, mode, **kw):
@@ -54,7 +56,8 @@ def golden():
         return json.load(f)
 
 
-@pytest.mark.parametrize("mi", range(7), ids=["exact", "b4", "b8", "b16", "b16_64", "b16_64_c2", "b8_128_c8"])
+@pytest.mark.parametrize("mi", range(9), ids=["exact", "b4", "b8", "b16", "b16_64", "b16_64_c2", "b8_128_c8",
+                                             "b16_64_lp", "b8_48_seq"])
 def test_golden_clusters(gpu_available, mi):
     from test_oracle import _cluster_from
     name, mode, kw = modes()[mi]
@@ -104,8 +107,9 @@ def test_tie_storm_chunk_cut(gpu_available, oracle_mod, kc):
                          alloc_pods=np.full(n, 110, np.int64), req_cpu=np.where(np.arange(p) % 3 == 0, 0, 200).astype(np.int64),
                          req_mem=np.where(np.arange(p) % 3 == 0, 0, 65536).astype(np.int64), req_pods=np.ones(p, np.int64))
     want = oracle_mod.schedule(cl)
-    for b in (64, 128):
-        assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=b, chunk_topk=kc), want, f"ties kc={kc} b={b}")
+    for b, impl in ((64, 0), (64, 2), (128, 0)):
+        assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=b, chunk_topk=kc, commit_impl=impl), want,
+                    f"ties kc={kc} b={b} impl={impl}")
 
 
 def test_exact_mode_workgroup_counts(gpu_available, oracle_mod):
@@ -174,7 +178,8 @@ def test_full_size_c3_batched_equals_exact(gpu_available):
     from ksched import MODE_BATCHED, MODE_EXACT, cluster
     cl = cluster.make_cluster("c3")
     a = run_engine(cl, MODE_EXACT)
-    for kw in (dict(topk=16, batch=128), dict(topk=16, batch=64), dict(topk=8, batch=32)):
+    for kw in (dict(topk=16, batch=128), dict(topk=16, batch=64), dict(topk=8, batch=32),
+               dict(topk=16, batch=64, commit_impl=2)):
         b = run_engine(cl, MODE_BATCHED, **kw)
         assert_same(b, a[:4], f"c3 full exact-vs-batched {kw}")
     oi = a[0]
