@@ -124,7 +124,8 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
         }
         return;
     }
-    const uint64_t t_start = __builtin_amdgcn_s_memtime();
+    const bool dbg = A.dbg != nullptr;  // diagnostics build of the phase timing (KSCHED_COMMIT_STAMPS)
+    const uint64_t t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t t_s1 = 0, t_s2 = 0, t_s3 = 0, t_mark = 0;
     SpcSmem m;
     {
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
     int32_t my_idx = 0, my_feas = 0;
     double my_score = 0.0;
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
-    int nT = nin, done = nb, round = 0, W = 64;
+    int nT = nin, done = nb, W = 64;
     int64_t placed = 0, nrounds = 0, nfail = 0;
     if (wave == 0) {
         fcc = pj ? (int32_t)(A.fc0[lane] + m.dfacc[lane]) : 0;
@@ -235,10 +236,10 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
     }
 
     int c = 0;
-    const uint64_t t_pro = __builtin_amdgcn_s_memtime() - t_start;
+    const uint64_t t_pro = dbg ? __builtin_amdgcn_s_memtime() - t_start : 0;
     for (;;) {
         // ---- step 1 (wave 0): guesses for pods [c, cend) ----
-        t_mark = __builtin_amdgcn_s_memtime();
+        if (dbg) t_mark = __builtin_amdgcn_s_memtime();
         if (wave == 0) {
             const int cend = (c + W < nb) ? c + W : nb;
             int ng = 0;
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
             if (lane == 0) { m.ctl[0] = c; m.ctl[1] = cend; }
         }
         __syncthreads();
-        { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s1 += t - t_mark; t_mark = t; }
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s1 += t - t_mark; t_mark = t; }
         const int rc0 = m.ctl[0], rce = m.ctl[1];
         // ---- step 2 (all waves): evaluate the guessed commits in parallel ----
         {
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
             m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
         }
         __syncthreads();
-        { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s2 += t - t_mark; t_mark = t; }
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s2 += t - t_mark; t_mark = t; }
         // ---- step 3 (wave 0): check, confirm the valid prefix, resolve the first failure ----
         if (wave == 0) {
             ++nrounds;
@@ -505,11 +506,10 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
                 W = 2 * W > 64 ? 64 : 2 * W;
                 c = cend;
             }
-            ++round;
             if (lane == 0) { m.ctl[0] = c; m.ctl[2] = (done < nb || c >= nb) ? 1 : 0; }
         }
         __syncthreads();
-        { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s3 += t - t_mark; t_mark = t; }
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s3 += t - t_mark; t_mark = t; }
         if (m.ctl[2]) break;
         c = m.ctl[0];
     }

@@ -49,7 +49,8 @@ struct ksched_ctx {
     int64_t *h_cursor = nullptr;  // pinned
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
     hipStream_t stream2 = nullptr;  // commit stream of the batched pipeline
-    hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_pipe[2] = {};
+    hipStream_t stream3 = nullptr;  // merge (+ rank exchange) stream of the batched pipeline
+    hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[2] = {};
     void *d_xring = nullptr, *d_lring = nullptr;
     int64_t xring_bytes = 0, lring_bytes = 0;
     // exact workspace
@@ -157,27 +158,24 @@ BatchPlan plan_batch(const ksched_ctx *c) {
     pl.B = c->B;
     pl.pod_groups = (pl.B + 63) / 64;
     const int64_t n = std::max<int64_t>(c->n_local, 1);
-    // enough waves to cover the chip (>= 8 waves per CU) while keeping >= 16 nodes per wave
+    // NSC sub-chunks (one wave each) in workgroups of kScoreWaves: 8 waves per CU at full size,
+    // >= KSCHED_MIN_CHUNK nodes per wave, <= merge_lists_max workgroups (the merge's register capacity)
     const int target_waves = env_int("KSCHED_TARGET_WAVES", c->cus * 8);
-    int64_t chunks = std::max<int64_t>(1, target_waves / pl.pod_groups);
+    int64_t nsc = std::max<int64_t>(1, target_waves / pl.pod_groups);
     const int min_s = env_int("KSCHED_MIN_CHUNK", 16);
-    chunks = std::min<int64_t>(chunks, (n + min_s - 1) / min_s);
-    chunks = std::min<int64_t>(chunks, 4096);
-    pl.S = (int)((n + chunks - 1) / chunks);
-    pl.n_chunks = (int)((n + pl.S - 1) / pl.S);
-    pl.C[0] = pl.n_chunks;
+    nsc = std::min<int64_t>(nsc, (n + min_s - 1) / min_s);
+    nsc = std::min<int64_t>(nsc, (int64_t)merge_lists_max(pl.KC) * kScoreWaves);
+    nsc = std::max<int64_t>(kScoreWaves, nsc / kScoreWaves * kScoreWaves);
+    pl.n_chunks = (int)nsc;
+    pl.S = (int)((n + nsc - 1) / nsc);
+    const int G = (int)(nsc / kScoreWaves);
+    pl.C[0] = G;
     pl.stages = 1;
-    while (pl.C[pl.stages - 1] > 64) {
-        pl.C[pl.stages] = (pl.C[pl.stages - 1] + 63) / 64;
-        pl.stages++;
-    }
     size_t off = 0;
     auto take = [&](size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; };
-    pl.off_part = take((size_t)pl.B * pl.n_chunks * pl.KC * sizeof(Cand));
-    pl.off_pcnt = take((size_t)pl.B * pl.n_chunks * sizeof(int64_t));
-    const int c1 = pl.stages > 1 ? pl.C[1] : 1;
-    pl.off_m1 = take((size_t)pl.B * c1 * pl.K * sizeof(Cand) * 2);  // ping-pong for stage >= 1
-    pl.off_m1cnt = take((size_t)pl.B * c1 * sizeof(int64_t) * 2);
+    pl.off_part = take((size_t)2 * pl.B * G * pl.KC * sizeof(Cand));  // ring of 2: score(b+1) || merge(b)
+    pl.off_pcnt = take((size_t)2 * pl.B * G * sizeof(int64_t));
+    pl.off_m1 = pl.off_m1cnt = 0;
     pl.send_bytes = (size_t)pl.B * pl.K * sizeof(Rec) + (size_t)pl.B * sizeof(int64_t);
     pl.off_send = take(pl.send_bytes);  // local lists + fc (also the single-GPU final lists)
     const int R = std::max(1, c->o.nranks);
@@ -242,7 +240,7 @@ int enqueue_batched(ksched_ctx *c) {
     if (impl != KSCHED_COMMIT_SEQUENTIAL && pl.B > 64) impl = KSCHED_COMMIT_SEQUENTIAL;
     const bool lp_commit = impl == KSCHED_COMMIT_LANE_PER_POD;
     const bool spc_commit = impl == KSCHED_COMMIT_SPECULATIVE;
-    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
+    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2, sM = one_stream ? c->stream : c->stream3;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -266,9 +264,10 @@ int enqueue_batched(ksched_ctx *c) {
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
     if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
-    if (!one_stream) {  // stream C starts after the initialisation above
+    if (!one_stream) {  // streams M and C start after the initialisation above
         HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));
         HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
+        HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
     }
     int64_t resolved = 0, b = 0, last_resolved_b = -1;
     double avg_progress = std::max(1.0, pl.B * 0.75);
@@ -288,53 +287,46 @@ int enqueue_batched(ksched_ctx *c) {
             ScoreArgs sa{};
             sa.nodes = c->d_nodes; sa.n_local = c->n_local; sa.node_offset = c->o.node_offset;
             sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = plan; sa.B = pl.B;
-            sa.part = reinterpret_cast<Cand *>(ws + pl.off_part);
-            sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt);
+            const size_t part_elems = (size_t)pl.B * pl.C[0];
+            sa.part = reinterpret_cast<Cand *>(ws + pl.off_part) + (size_t)(b % 2) * part_elems * pl.KC;
+            sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt) + (size_t)(b % 2) * part_elems;
             sa.patch = xbuf(b - 2);
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
             HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
-            HIPCHK(c, ev_begin(c, tm, &e0, sS));
-            const void *in = sa.part;
-            const int64_t *in_cnt = sa.part_cnt;
-            for (int st = 0; st < pl.stages; ++st) {
+            // M: merge b while stream S scores b+1 (the lists' part buffers alternate)
+            if (!one_stream) {
+                HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
+                HIPCHK(c, hipStreamWaitEvent(sM, c->ev_scored[b % kRing], 0));
+            }
+            HIPCHK(c, ev_begin(c, tm, &e0, sM));
+            {
                 MergeArgs ma{};
-                ma.in = in; ma.in_cnt = in_cnt; ma.C_in = pl.C[st];
-                ma.chunk_input = st == 0 ? 1 : 0;
-                ma.C_out = (pl.C[st] + 63) / 64;
+                ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
-                const bool fin = (st == pl.stages - 1);
-                if (fin) {
-                    ma.out_rec = reinterpret_cast<Rec *>(lists_base);
-                    ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
-                } else {
-                    const int pp = st & 1;
-                    const int c1 = pl.C[1];
-                    ma.out = reinterpret_cast<Cand *>(ws + pl.off_m1) + (size_t)pp * pl.B * c1 * pl.K;
-                    ma.out_cnt = reinterpret_cast<int64_t *>(ws + pl.off_m1cnt) + (size_t)pp * pl.B * c1;
-                }
-                HIPCHK(c, launch_merge(st == 0 ? pl.KC : pl.K, pl.K, false, fin, ma, sS));
-                in = ma.out; in_cnt = ma.out_cnt;
+                ma.out_rec = reinterpret_cast<Rec *>(lists_base);
+                ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
+                HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sM));
             }
-            HIPCHK(c, ev_end(c, tm, 1, e0, 0, sS));
+            HIPCHK(c, ev_end(c, tm, 1, e0, 0, sM));
             const Rec *lists = reinterpret_cast<const Rec *>(lists_base);
             const int64_t *fc0 = reinterpret_cast<const int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
             if (c->comm) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
-                HIPCHK(c, ev_begin(c, tm, &e0, sS));
-                NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sS));
+                HIPCHK(c, ev_begin(c, tm, &e0, sM));
+                NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sM));
                 MergeArgs ma{};
                 ma.in = ws + pl.off_recv; ma.rank_stride = (int64_t)pl.send_bytes; ma.C_in = R; ma.C_out = 1;
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists) + (size_t)(b % 2) * pl.B * pl.K;
                 ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc) + (size_t)(b % 2) * pl.B;
-                HIPCHK(c, launch_merge(pl.K, pl.K, true, true, ma, sS));
+                HIPCHK(c, launch_merge(pl.K, pl.K, true, true, ma, sM));
                 lists = ma.out_rec;
                 fc0 = ma.out_fc;
-                HIPCHK(c, ev_end(c, tm, 3, e0, 0, sS));
+                HIPCHK(c, ev_end(c, tm, 3, e0, 0, sM));
             }
             if (!one_stream) {
-                HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sS));
+                HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sM));
                 HIPCHK(c, hipStreamWaitEvent(sC, c->ev_lists[b % kRing], 0));
             }
             // C: ordered commit of batch b
@@ -491,10 +483,12 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     bool ev_ok = true;
     for (int i = 0; i < 4; ++i)
         ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_lists[i], hipEventDisableTiming) == hipSuccess &&
-                hipEventCreateWithFlags(&c->ev_commit[i], hipEventDisableTiming) == hipSuccess;
+                hipEventCreateWithFlags(&c->ev_commit[i], hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&c->ev_scored[i], hipEventDisableTiming) == hipSuccess;
     for (int i = 0; i < 2; ++i) ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming) == hipSuccess;
     if (!ev_ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc((void **)&c->d_cursor, sizeof(Ctl)) != hipSuccess ||
         hipMalloc((void **)&c->d_err, sizeof(int32_t)) != hipSuccess ||
@@ -515,6 +509,7 @@ int ksched_destroy(ksched_ctx *c) {
     hipSetDevice(c->dev);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->stream2) hipStreamSynchronize(c->stream2);
+    if (c->stream3) hipStreamSynchronize(c->stream3);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
@@ -527,11 +522,13 @@ int ksched_destroy(ksched_ctx *c) {
     for (int i = 0; i < 4; ++i) {
         if (c->ev_lists[i]) hipEventDestroy(c->ev_lists[i]);
         if (c->ev_commit[i]) hipEventDestroy(c->ev_commit[i]);
+        if (c->ev_scored[i]) hipEventDestroy(c->ev_scored[i]);
     }
     for (int i = 0; i < 2; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
+    if (c->stream3) hipStreamDestroy(c->stream3);
     delete c;
     return KSCHED_OK;
 }

@@ -89,13 +89,13 @@ struct ScoreArgs {
     NodeRec *nodes;    // read; the rows of `patch` are written back by their chunk's wave
     int64_t n_local;
     int64_t node_offset;
-    int32_t S;         // nodes per chunk (one wave per chunk and 64 pods)
-    int32_t n_chunks;
+    int32_t S;         // unused
+    int32_t n_chunks;  // NSC sub-chunks = workgroups x kScoreWaves
     PodArgs pods;
     const int64_t *cursor;  // this batch's plan slot (first pod, or -1)
     int32_t B;
-    Cand *part;        // [B][n_chunks][KC]
-    int64_t *part_cnt; // [B][n_chunks]
+    Cand *part;        // [B][workgroups][KC]
+    int64_t *part_cnt; // [B][workgroups]
     const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
 };
 
@@ -192,6 +192,8 @@ hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool fast53, const
                         bool cooperative, hipStream_t s);
 hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
                              hipStream_t s);
+// one workgroup per pod: the score kernel's workgroup lists -> the pod's K-entry Rec list (C_in <= 256)
+hipError_t launch_merge_pod(int KC, int K, const MergeArgs &a, hipStream_t s);
 hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s);
 hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, size_t lds_bytes,
                          hipStream_t s);
@@ -207,6 +209,13 @@ hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, doub
                                hipStream_t s);
 
 constexpr int kExactBlock = 256;
+
+// score kernel geometry: 4 waves per workgroup, 2 workgroups per CU at the default grid
+constexpr int kScoreWaves = 4;
+// merge: one wave per pod holding every workgroup list in registers (<= 32 entries per lane)
+constexpr int merge_lists_max(int KC) { return KC <= 4 ? 512 : 64 * 32 / KC; }
+constexpr int kScoreThreads = kScoreWaves * 64;
+constexpr size_t score_lds_bytes(int KC) { return (size_t)(kScoreWaves / 2) * KC * 64 * 12 + 64 * 4; }
 
 // (priority, domain, labels, fast53) -> instantiation.  Best-price always ranges over feasible nodes
 // and never divides (fast53 irrelevant).

@@ -195,32 +195,53 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Batched mode, stage 1: fused predicate + score + per-lane top-KC.  Lane = pod of the batch, wave =
-// one node chunk; node rows are wave-uniform (scalar loads of the 96-B NodeRec, reciprocals included).
-// Chunk c holds the nodes c, c + C, c + 2C, ... (strided): nodes tied on key rank by index, so a
-// strided split spreads the lowest-index ties over all chunks and short chunk lists still merge into a
-// long exact prefix.  A chunk list is "cut" when it holds KC entries (more candidates may exist, all
-// ranking below its last entry); the merge turns that into an exact valid prefix per pod.
-// The list is kept sorted by (key desc, idx asc) with a branch-free register insert.
+// Batched mode, stage 1: fused predicate + score + top-KC per (pod, workgroup).  Lane = pod of the
+// batch.  A workgroup is kScoreWaves waves; wave w of workgroup g scans sub-chunk s = g + G*w of the
+// NSC = G*kScoreWaves sub-chunks, i.e. the nodes j with j mod NSC == s: workgroup g holds the nodes
+// j = g (mod G), so the lowest-index members of a tie class land in different workgroups and short
+// lists still merge into a long exact prefix.  Node rows are wave-uniform (scalar loads of the 96-B
+// NodeRec, reciprocals included).
+//   Each wave keeps a sorted top-KC per lane (branch-free register insert; nodes arrive in ascending
+//   index, so a strict key compare keeps ties in index order).  The wave lists fold pairwise through
+//   LDS into one list per (pod, workgroup): two lists that are each cut when full fold into the top-KC
+//   of their union, again cut when full.
 // ------------------------------------------------------------------------------------------------
+template <int KC>
+__device__ __forceinline__ void list_insert_ordered(double (&key)[KC], int32_t (&idx)[KC], double ck, int32_t ci) {
+    bool moved = false;  // once placed, every later entry shifts down one slot
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+        const bool sw = moved || better(ck, ci, key[q], idx[q]);
+        moved = sw;
+        const double tk = key[q];
+        const int32_t ti = idx[q];
+        key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+        ck = sw ? tk : ck; ci = sw ? ti : ci;
+    }
+}
+
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
+__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    double *s_key = reinterpret_cast<double *>(smem);                                   // [W/2][KC][64]
+    int32_t *s_idx = reinterpret_cast<int32_t *>(smem + (size_t)(kScoreWaves / 2) * KC * 64 * 8);
+    int32_t *s_cnt = s_idx + (size_t)(kScoreWaves / 2) * KC * 64;                        // [64]
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int chunk = blockIdx.x * 4 + wave;
-    if (chunk >= A.n_chunks) return;
-    const int64_t C = A.n_chunks;
-    // Batch b-2's commits (<= 128 nodes, two per lane): this wave owns the ones in its chunk.  It
-    // writes them back to the rows (for the next launches) and overlays them on what it reads in this
-    // launch, so no separate apply kernel has to run between commit(b-2) and score(b).
-    int64_t pj0 = -1, pj1 = -1;  // local node index of entries lane and lane + 64, if in this chunk
+    const int64_t G = gridDim.x;
+    const int64_t NSC = G * kScoreWaves;
+    const int64_t sub = (int64_t)blockIdx.x + G * wave;
+    // Batch b-2's commits (<= 128 nodes, two per lane): the wave whose sub-chunk holds a node writes it
+    // back to the row (for the next launches) and overlays it on what it reads in this launch, so no
+    // separate apply kernel has to run between commit(b-2) and score(b).
+    int64_t pj0 = -1, pj1 = -1;  // local node index of entries lane and lane + 64, if in this sub-chunk
     {
         const int np = A.patch->count;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int e = h * 64 + lane;
             const int64_t j = e < np ? (int64_t)A.patch->e[e].idx - A.node_offset : -1;
-            const bool mine = j >= 0 && j < A.n_local && (j % C) == chunk;
+            const bool mine = j >= 0 && j < A.n_local && (j % NSC) == sub;
             if (mine && blockIdx.y == 0) {
                 const XRec &x = A.patch->e[e];
                 set_node(A.nodes + j, x.cur[0], x.cur[1], x.cur[2]);
@@ -230,8 +251,10 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
         }
     }
     const bool anyp = __ballot(pj0 >= 0 || pj1 >= 0) != 0;
+    if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0;
     const int64_t p0 = *A.cursor;
-    if (p0 < 0 || p0 >= A.pods.p) return;
+    if (p0 < 0 || p0 >= A.pods.p) return;  // workgroup-uniform
+    __syncthreads();
     const int b = blockIdx.y * 64 + lane;
     const int64_t pod = p0 + b;
     const bool active = (b < A.B) && (pod < A.pods.p);
@@ -246,12 +269,12 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
     int32_t idx[KC];
 #pragma unroll
     for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
-    int64_t cnt = 0;
-    for (int64_t j = chunk; j < A.n_local; j += C) {
+    int32_t cnt = 0;
+    for (int64_t j = sub; j < A.n_local; j += NSC) {
         const NodeRec &nd = A.nodes[j];
         int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
         double af0 = nd.af[0], af1 = nd.af[1], af2 = nd.af[2], y0 = nd.y[0], y1 = nd.y[1], y2 = nd.y[2];
-        if (anyp) {  // wave-uniform: this chunk holds committed nodes of batch b-2
+        if (anyp) {  // wave-uniform: this sub-chunk holds committed nodes of batch b-2
             const uint64_t hit = __ballot(pj0 == j || pj1 == j);
             if (hit) {
                 const int src = __ffsll((unsigned long long)hit) - 1;
@@ -265,8 +288,6 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
         const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
         cnt += f;
         double k;
-        // Nodes arrive in ascending index, so a newcomer loses every tie: a strict key compare keeps
-        // the list in (key desc, idx asc) order (empty slots hold -inf and never beat a real key).
         const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, af0, af1, af2, y0, y1,
                                                       y2, y3, nd.price, &k);
         double ck = el ? k : -__builtin_inf();
@@ -282,11 +303,143 @@ __global__ __launch_bounds__(256) void k_score_topk(ScoreArgs A) {
             ck = sw ? tk : ck; ci = sw ? ti : ci;
         }
     }
-    if (!active) return;
-    Cand *dst = A.part + ((size_t)b * A.n_chunks + chunk) * KC;
+    if (cnt) atomicAdd(&s_cnt[lane], cnt);
+    // fold the wave lists pairwise: W -> W/2 -> ... -> 1
 #pragma unroll
-    for (int q = 0; q < KC; ++q) { dst[q].key = key[q]; dst[q].idx = idx[q]; dst[q].pad = 0; }
-    A.part_cnt[(size_t)b * A.n_chunks + chunk] = cnt;
+    for (int half = kScoreWaves / 2; half >= 1; half >>= 1) {
+        if (wave >= half && wave < 2 * half) {
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+                s_key[((wave - half) * KC + q) * 64 + lane] = key[q];
+                s_idx[((wave - half) * KC + q) * 64 + lane] = idx[q];
+            }
+        }
+        __syncthreads();
+        if (wave < half) {
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+                const int32_t oi = s_idx[(wave * KC + q) * 64 + lane];
+                if (oi == kNoIdx) break;
+                list_insert_ordered<KC>(key, idx, s_key[(wave * KC + q) * 64 + lane], oi);
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 0 && active) {
+        Cand *dst = A.part + ((size_t)b * G + blockIdx.x) * KC;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) { dst[q].key = key[q]; dst[q].idx = idx[q]; dst[q].pad = 0; }
+        A.part_cnt[(size_t)b * G + blockIdx.x] = s_cnt[lane];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Merge of one pod's workgroup lists (C_in <= 64*LPL lists of KC entries, cut when full) into its
+// K-entry Rec list: ONE wave per pod, lane l holding lists l*LPL .. l*LPL+LPL-1 in registers with a
+// head per list and the lane's best head cached.  K rounds of wave arg-best (64-bit order-preserving
+// max, ties by node index) pop the winning lane's head.  Exact prefix: the result keeps only entries
+// ranking at or above the best cutoff (the last entry of every cut input list) and is cut (flag in
+// entry 0's pad) when any input was cut or entries were left over.
+// ------------------------------------------------------------------------------------------------
+template <int KC, int K, int LPL>
+__global__ __launch_bounds__(64) void k_merge_pod(MergeArgs A) {
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const int64_t p0 = *A.cursor;
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;
+    double key[LPL][KC];
+    int32_t idx[LPL][KC];
+    int hd[LPL];
+    int64_t cnt = 0;
+    double ck = -__builtin_inf();  // best cutoff among this lane's cut lists
+    int32_t ci = kNoIdx;
+    bool anycut = false;
+#pragma unroll
+    for (int u = 0; u < LPL; ++u) {
+        const int list = lane * LPL + u;
+        const bool has = list < A.C_in;
+        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? list : 0)) * KC;
+        int n = 0;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            key[u][q] = has ? src[q].key : -__builtin_inf();
+            idx[u][q] = has ? src[q].idx : kNoIdx;
+            n += idx[u][q] != kNoIdx;
+        }
+        hd[u] = 0;
+        if (has) cnt += A.in_cnt[(size_t)b * A.C_in + list];
+        if (n == KC) {  // a full list may hide candidates ranking below its last entry
+            anycut = true;
+            if (ci == kNoIdx || better(key[u][KC - 1], idx[u][KC - 1], ck, ci)) { ck = key[u][KC - 1]; ci = idx[u][KC - 1]; }
+        }
+    }
+    {
+        int32_t cs = lane;
+        wave_argbest_fast(ck, ci, cs);
+    }
+    cnt = wave_sum_i64(cnt);
+    const bool gcut = __ballot(anycut) != 0;
+    // cached head of every list, and the lane's best head
+    double hk[LPL];
+    int32_t hi[LPL];
+#pragma unroll
+    for (int u = 0; u < LPL; ++u) { hk[u] = key[u][0]; hi[u] = idx[u][0]; }
+    double bk = hk[0];
+    int32_t bi = hi[0];
+    int bu = 0;
+#pragma unroll
+    for (int u = 1; u < LPL; ++u) {
+        const bool up = hi[u] != kNoIdx && (bi == kNoIdx || better(hk[u], hi[u], bk, bi));
+        bk = up ? hk[u] : bk; bi = up ? hi[u] : bi; bu = up ? u : bu;
+    }
+    double mk = -__builtin_inf();
+    int32_t mi = kNoIdx;
+    for (int r = 0; r < K; ++r) {
+        double wk = bk;
+        int32_t wi = bi, ws = lane;
+        wave_argbest_fast(wk, wi, ws);
+        if (wi == kNoIdx) break;  // wave-uniform
+        if (lane == r) { mk = wk; mi = wi; }
+        if (lane == ws) {  // pop the winning list's head
+#pragma unroll
+            for (int u = 0; u < LPL; ++u) {
+                if (u == bu) {
+                    const int h = ++hd[u];
+                    double nk = -__builtin_inf();
+                    int32_t ni = kNoIdx;
+#pragma unroll
+                    for (int q = 1; q < KC; ++q) {
+                        nk = (q == h) ? key[u][q] : nk;
+                        ni = (q == h) ? idx[u][q] : ni;
+                    }
+                    hk[u] = nk; hi[u] = ni;
+                }
+            }
+            bk = hk[0]; bi = hi[0]; bu = 0;
+#pragma unroll
+            for (int u = 1; u < LPL; ++u) {
+                const bool up = hi[u] != kNoIdx && (bi == kNoIdx || better(hk[u], hi[u], bk, bi));
+                bk = up ? hk[u] : bk; bi = up ? hi[u] : bi; bu = up ? u : bu;
+            }
+        }
+    }
+    const bool left = __ballot(bi != kNoIdx) != 0;  // candidates beyond the K output entries
+    if (ci != kNoIdx && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
+    const int32_t cut_out = (gcut || left) ? 1 : 0;
+    if (lane < K) {
+        Rec r{};
+        if (mi != kNoIdx) {
+            const NodeRec &nd = A.nodes[mi - A.node_offset];
+            r.key = mk; r.idx = mi; r.valid = 1;
+            r.a[0] = nd.a[0]; r.a[1] = nd.a[1]; r.a[2] = nd.a[2];
+            r.labels = nd.labels; r.price = nd.price;
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        r.pad = lane == 0 ? cut_out : 0;
+        A.out_rec[(size_t)b * K + lane] = r;
+    }
+    if (lane == 0) A.out_fc[b] = cnt;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -813,8 +966,16 @@ hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStrea
 
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
 hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
-    dim3 grid((a.n_chunks + 3) / 4, pod_groups);
-    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53>), grid, dim3(256), 0, s, a);
+    const size_t lds = score_lds_bytes(KC);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_score_topk<KC, PRIO, DOM, LAB, F53>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    dim3 grid((unsigned)(a.n_chunks / kScoreWaves), pod_groups);
+    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53>), grid, dim3(kScoreThreads), lds, s, a);
     return hipGetLastError();
 }
 
@@ -902,6 +1063,42 @@ hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const 
         case 4: return merge_k<4>(KIN, input_rec, final_stage, a, s);
         case 8: return merge_k<8>(KIN, input_rec, final_stage, a, s);
         case 16: return merge_k<16>(KIN, input_rec, final_stage, a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+namespace {
+template <int KC, int K>
+hipError_t merge_pod_l(const MergeArgs &a, hipStream_t s) {
+    // lists per lane; LPL * KC <= 32 register entries per lane (merge_lists_max)
+    const int lpl = (a.C_in + 63) / 64;
+    if (lpl > merge_lists_max(KC) / 64) return hipErrorInvalidValue;
+    if (lpl <= 1) hipLaunchKernelGGL((k_merge_pod<KC, K, 1>), dim3(a.B), dim3(64), 0, s, a);
+    else if (lpl <= 2) hipLaunchKernelGGL((k_merge_pod<KC, K, 2>), dim3(a.B), dim3(64), 0, s, a);
+    else if constexpr (KC <= 8) {
+        if (lpl <= 4) hipLaunchKernelGGL((k_merge_pod<KC, K, 4>), dim3(a.B), dim3(64), 0, s, a);
+        else if constexpr (KC <= 4) hipLaunchKernelGGL((k_merge_pod<KC, K, 8>), dim3(a.B), dim3(64), 0, s, a);
+    }
+    return hipGetLastError();
+}
+template <int K>
+hipError_t merge_pod_k(int KC, const MergeArgs &a, hipStream_t s) {
+    switch (KC) {
+        case 2: return merge_pod_l<2, K>(a, s);
+        case 4: return merge_pod_l<4, K>(a, s);
+        case 8: return merge_pod_l<8, K>(a, s);
+        case 16: return merge_pod_l<16, K>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+hipError_t launch_merge_pod(int KC, int K, const MergeArgs &a, hipStream_t s) {
+    if (a.C_in > merge_lists_max(KC) || KC > K) return hipErrorInvalidValue;
+    switch (K) {
+        case 4: return merge_pod_k<4>(KC, a, s);
+        case 8: return merge_pod_k<8>(KC, a, s);
+        case 16: return merge_pod_k<16>(KC, a, s);
         default: return hipErrorInvalidValue;
     }
 }
