@@ -76,6 +76,7 @@ __device__ __forceinline__ uint64_t lp_stamp() {
 
 template <int K, int PRIO, int DOM, bool LAB, bool F53, bool ST>
 __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;

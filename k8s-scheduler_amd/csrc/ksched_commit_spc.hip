@@ -109,6 +109,7 @@ __device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64
 
 template <int K, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
     const int lane = tid & 63;

@@ -48,6 +48,7 @@ struct ksched_ctx {
     int64_t *d_cursor = nullptr;  // [0] cursor, [1..3] stats
     int64_t *h_cursor = nullptr;  // pinned
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
+    int64_t *d_mdbg = nullptr;    // KSCHED_MERGE_STAMPS diagnostics
     hipStream_t stream2 = nullptr;  // commit stream of the batched pipeline
     hipStream_t stream3 = nullptr;  // merge (+ rank exchange) stream of the batched pipeline
     hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[2] = {};
@@ -159,12 +160,12 @@ BatchPlan plan_batch(const ksched_ctx *c) {
     pl.pod_groups = (pl.B + 63) / 64;
     const int64_t n = std::max<int64_t>(c->n_local, 1);
     // NSC sub-chunks (one wave each) in workgroups of kScoreWaves: 8 waves per CU at full size,
-    // >= KSCHED_MIN_CHUNK nodes per wave, <= merge_lists_max workgroups (the merge's register capacity)
+    // >= KSCHED_MIN_CHUNK nodes per wave, <= kMergeThreads workgroups (one merge lane per list)
     const int target_waves = env_int("KSCHED_TARGET_WAVES", c->cus * 8);
     int64_t nsc = std::max<int64_t>(1, target_waves / pl.pod_groups);
     const int min_s = env_int("KSCHED_MIN_CHUNK", 16);
     nsc = std::min<int64_t>(nsc, (n + min_s - 1) / min_s);
-    nsc = std::min<int64_t>(nsc, (int64_t)merge_lists_max(pl.KC) * kScoreWaves);
+    nsc = std::min<int64_t>(nsc, (int64_t)kMergeThreads * kScoreWaves);
     nsc = std::max<int64_t>(kScoreWaves, nsc / kScoreWaves * kScoreWaves);
     pl.n_chunks = (int)nsc;
     pl.S = (int)((n + nsc - 1) / nsc);
@@ -264,6 +265,8 @@ int enqueue_batched(ksched_ctx *c) {
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
     if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
+    if (env_int("KSCHED_MERGE_STAMPS", 0) && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
+    if (c->d_mdbg) HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), sS));
     if (!one_stream) {  // streams M and C start after the initialisation above
         HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));
         HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
@@ -305,6 +308,7 @@ int enqueue_batched(ksched_ctx *c) {
                 ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
+                ma.dbg = c->d_mdbg;
                 ma.out_rec = reinterpret_cast<Rec *>(lists_base);
                 ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
                 HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sM));
@@ -361,6 +365,15 @@ int enqueue_batched(ksched_ctx *c) {
     if (!one_stream) {  // the run's end event is recorded on stream S: make it cover stream C
         HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));
         HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
+    }
+    if (c->d_mdbg) {
+        int64_t hm[8];
+        HIPCHK(c, hipStreamSynchronize(sS));
+        HIPCHK(c, hipMemcpy(hm, c->d_mdbg, sizeof(hm), hipMemcpyDeviceToHost));
+        const double nwg = hm[7] ? (double)hm[7] : 1.0;
+        std::fprintf(stderr, "[ksched merge stamps] workgroups=%lld | cycles/wg: loads %.0f rank-heads %.0f barrier %.0f "
+                     "global-heads %.0f rank-entries %.0f write %.0f\n", (long long)hm[7], hm[0] / nwg, hm[1] / nwg,
+                     hm[2] / nwg, hm[3] / nwg, hm[4] / nwg, hm[5] / nwg);
     }
     const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
     c->st.batches = h->stats[0];
@@ -514,7 +527,7 @@ int ksched_destroy(ksched_ctx *c) {
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
     hipFree(c->d_oidx); hipFree(c->d_osc); hipFree(c->d_ofeas);
-    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_dbg); hipFree(c->d_slots); hipFree(c->d_err);
+    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_dbg); hipFree(c->d_mdbg); hipFree(c->d_slots); hipFree(c->d_err);
     if (c->h_cursor) hipHostFree(c->h_cursor);
     for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);

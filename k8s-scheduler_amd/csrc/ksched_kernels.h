@@ -107,6 +107,7 @@ struct MergeArgs {
     int32_t C_in;
     int32_t C_out;          // ceil(C_in / 64)
     int32_t chunk_input;    // 1: inputs are score-kernel chunk lists (cut when full)
+    int64_t *dbg;           // diagnostics only (KSCHED_MERGE_STAMPS): per-phase cycle sums, else null
     Cand *out;              // [B][C_out][K] (non-final)
     int64_t *out_cnt;       // [B][C_out]
     Rec *out_rec;           // [B][K]  (final)
@@ -212,8 +213,7 @@ constexpr int kExactBlock = 256;
 
 // score kernel geometry: 4 waves per workgroup, 2 workgroups per CU at the default grid
 constexpr int kScoreWaves = 4;
-// merge: one wave per pod holding every workgroup list in registers (<= 32 entries per lane)
-constexpr int merge_lists_max(int KC) { return KC <= 4 ? 512 : 64 * 32 / KC; }
+constexpr int kMergeThreads = 512;  // merge: one workgroup per pod, lane = one workgroup list (<= 512)
 constexpr int kScoreThreads = kScoreWaves * 64;
 constexpr size_t score_lds_bytes(int KC) { return (size_t)(kScoreWaves / 2) * KC * 64 * 12 + 64 * 4; }
 

@@ -334,103 +334,164 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Merge of one pod's workgroup lists (C_in <= 64*LPL lists of KC entries, cut when full) into its
-// K-entry Rec list: ONE wave per pod, lane l holding lists l*LPL .. l*LPL+LPL-1 in registers with a
-// head per list and the lane's best head cached.  K rounds of wave arg-best (64-bit order-preserving
-// max, ties by node index) pop the winning lane's head.  Exact prefix: the result keeps only entries
-// ranking at or above the best cutoff (the last entry of every cut input list) and is cut (flag in
-// entry 0's pad) when any input was cut or entries were left over.
+// Merge of one pod's workgroup lists (C_in <= 512 lists of KC entries, cut when full) into its K-entry
+// Rec list: one 512-thread workgroup per pod, thread = list.  Selection by RANK, every compare
+// independent (broadcast LDS reads of order-preserving 64-bit key codes; no serial rounds):
+//   1. each list head is ranked within its wave; the K best heads of each wave survive;
+//   2. the <= 8K survivors are ranked against each other; the K best heads' lists are kept -- every
+//      entry of the pod's top K lies in one of them (K better heads exist for any entry outside them);
+//   3. the kept lists' K*KC entries are ranked against each other; rank < K is the output position.
+// Exact prefix: the result keeps only entries ranking at or above the best cutoff (the last entry of
+// every cut input list) and is cut (flag in entry 0's pad) when any input was cut or entries were left
+// over.
 // ------------------------------------------------------------------------------------------------
-template <int KC, int K, int LPL>
-__global__ __launch_bounds__(64) void k_merge_pod(MergeArgs A) {
-    const int lane = threadIdx.x;
+__device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb, int32_t ib) {
+    return ca > cb || (ca == cb && ia < ib);
+}
+
+template <int KC, int K>
+__global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    constexpr int W = kMergeThreads / 64;
+    __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
+    __shared__ int32_t s_idx[kMergeThreads][KC];
+    __shared__ uint64_t s_ccode[W * K];             // surviving heads
+    __shared__ int32_t s_cidx[W * K], s_clist[W * K];
+    __shared__ int32_t s_keep[K];                   // list of global head rank g
+    __shared__ uint64_t s_ocode[K];
+    __shared__ int32_t s_oidx[K];
+    __shared__ uint64_t s_wck[W];
+    __shared__ int32_t s_wci[W], s_wcut[W], s_wnv[W];
+    __shared__ int64_t s_wcnt[W];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int b = blockIdx.x;
+    const bool dbg = A.dbg != nullptr;
+    uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
     const int64_t p0 = *A.cursor;
-    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;
-    double key[LPL][KC];
-    int32_t idx[LPL][KC];
-    int hd[LPL];
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // workgroup-uniform
+    const bool has = tid < A.C_in;
+    uint64_t code[KC];
+    int32_t idx[KC];
+    int n = 0;
     int64_t cnt = 0;
-    double ck = -__builtin_inf();  // best cutoff among this lane's cut lists
-    int32_t ci = kNoIdx;
-    bool anycut = false;
-#pragma unroll
-    for (int u = 0; u < LPL; ++u) {
-        const int list = lane * LPL + u;
-        const bool has = list < A.C_in;
-        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? list : 0)) * KC;
-        int n = 0;
+    {
+        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? tid : 0)) * KC;
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
-            key[u][q] = has ? src[q].key : -__builtin_inf();
-            idx[u][q] = has ? src[q].idx : kNoIdx;
-            n += idx[u][q] != kNoIdx;
+            const int32_t x = has ? src[q].idx : kNoIdx;
+            idx[q] = x;
+            code[q] = x == kNoIdx ? 0ull : key_code(src[q].key);
+            n += x != kNoIdx;
         }
-        hd[u] = 0;
-        if (has) cnt += A.in_cnt[(size_t)b * A.C_in + list];
-        if (n == KC) {  // a full list may hide candidates ranking below its last entry
-            anycut = true;
-            if (ci == kNoIdx || better(key[u][KC - 1], idx[u][KC - 1], ck, ci)) { ck = key[u][KC - 1]; ci = idx[u][KC - 1]; }
-        }
+        if (has) cnt = A.in_cnt[(size_t)b * A.C_in + tid];
     }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { s_code[tid][q] = code[q]; s_idx[tid][q] = idx[q]; }
+    if (dbg) { asm volatile("" ::"v"(code[0]), "v"(cnt)); ts[1] = __builtin_amdgcn_s_memtime(); }
+    // wave partials: best cutoff (last entry of a full list), count, cut flag
     {
-        int32_t cs = lane;
-        wave_argbest_fast(ck, ci, cs);
+        const bool cut = n == KC;
+        uint64_t ck = cut ? code[KC - 1] : 0ull;
+        int32_t ci = cut ? idx[KC - 1] : kNoIdx;
+        const uint64_t bc = wave_max_u64(ck);
+        const int32_t bi = wave_min_i32((ck == bc && ci != kNoIdx) ? ci : kNoIdx);
+        const int64_t wc = wave_sum_i64(cnt);
+        const bool wcut = __ballot(cut) != 0;
+        const int nv = __popcll(__ballot(idx[0] != kNoIdx));
+        if (lane == 0) { s_wck[wave] = bc; s_wci[wave] = bi; s_wcut[wave] = wcut; s_wcnt[wave] = wc; s_wnv[wave] = nv; }
     }
-    cnt = wave_sum_i64(cnt);
-    const bool gcut = __ballot(anycut) != 0;
-    // cached head of every list, and the lane's best head
-    double hk[LPL];
-    int32_t hi[LPL];
-#pragma unroll
-    for (int u = 0; u < LPL; ++u) { hk[u] = key[u][0]; hi[u] = idx[u][0]; }
-    double bk = hk[0];
-    int32_t bi = hi[0];
-    int bu = 0;
-#pragma unroll
-    for (int u = 1; u < LPL; ++u) {
-        const bool up = hi[u] != kNoIdx && (bi == kNoIdx || better(hk[u], hi[u], bk, bi));
-        bk = up ? hk[u] : bk; bi = up ? hi[u] : bi; bu = up ? u : bu;
-    }
-    double mk = -__builtin_inf();
-    int32_t mi = kNoIdx;
-    for (int r = 0; r < K; ++r) {
-        double wk = bk;
-        int32_t wi = bi, ws = lane;
-        wave_argbest_fast(wk, wi, ws);
-        if (wi == kNoIdx) break;  // wave-uniform
-        if (lane == r) { mk = wk; mi = wi; }
-        if (lane == ws) {  // pop the winning list's head
-#pragma unroll
-            for (int u = 0; u < LPL; ++u) {
-                if (u == bu) {
-                    const int h = ++hd[u];
-                    double nk = -__builtin_inf();
-                    int32_t ni = kNoIdx;
-#pragma unroll
-                    for (int q = 1; q < KC; ++q) {
-                        nk = (q == h) ? key[u][q] : nk;
-                        ni = (q == h) ? idx[u][q] : ni;
-                    }
-                    hk[u] = nk; hi[u] = ni;
-                }
-            }
-            bk = hk[0]; bi = hi[0]; bu = 0;
-#pragma unroll
-            for (int u = 1; u < LPL; ++u) {
-                const bool up = hi[u] != kNoIdx && (bi == kNoIdx || better(hk[u], hi[u], bk, bi));
-                bk = up ? hk[u] : bk; bi = up ? hi[u] : bi; bu = up ? u : bu;
-            }
+    __syncthreads();
+    // 1. rank each head within its wave (broadcast reads, independent compares)
+    {
+        int rank = 0;
+        const int base = wave * 64;
+#pragma unroll 16
+        for (int t = 0; t < 64; ++t)
+            rank += code_better(s_code[base + t][0], s_idx[base + t][0], code[0], idx[0]) ? 1 : 0;
+        if (idx[0] != kNoIdx && rank < K) {
+            s_ccode[wave * K + rank] = code[0];
+            s_cidx[wave * K + rank] = idx[0];
+            s_clist[wave * K + rank] = tid;
         }
     }
-    const bool left = __ballot(bi != kNoIdx) != 0;  // candidates beyond the K output entries
-    if (ci != kNoIdx && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
+    if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
+    // 2. rank the survivors against each other
+    const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
+    int ntot = 0;  // valid heads in total (survivors: the first min(K, nv) slots of each wave)
+    for (int w = 0; w < nw; ++w) ntot += s_wnv[w];
+    if (tid < nw * K) {
+        const int w = tid / K, p = tid % K;
+        const int nvw = s_wnv[w] < K ? s_wnv[w] : K;
+        if (p < nvw) {
+            const uint64_t mc = s_ccode[tid];
+            const int32_t mi = s_cidx[tid];
+            int g = 0;
+            for (int w2 = 0; w2 < nw; ++w2) {
+                const int nv2 = s_wnv[w2] < K ? s_wnv[w2] : K;
+#pragma unroll 8
+                for (int p2 = 0; p2 < K; ++p2)
+                    g += (p2 < nv2 && code_better(s_ccode[w2 * K + p2], s_cidx[w2 * K + p2], mc, mi)) ? 1 : 0;
+            }
+            if (g < K) s_keep[g] = s_clist[tid];
+        }
+    }
+    if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    // 3. rank the kept lists' entries against each other
+    const int nkeep = ntot < K ? ntot : K;
+    const int ne = nkeep * KC;
+    int nvalid = 0;
+    if (tid < ne) {
+        const int l = s_keep[tid / KC], q = tid % KC;
+        const uint64_t mc = s_code[l][q];
+        const int32_t mi = s_idx[l][q];
+        if (mi != kNoIdx) {
+            int r = 0;
+            for (int e = 0; e < ne; ++e) {
+                const int l2 = s_keep[e / KC], q2 = e % KC;
+                r += code_better(s_code[l2][q2], s_idx[l2][q2], mc, mi) ? 1 : 0;
+            }
+            if (r < K) { s_ocode[r] = mc; s_oidx[r] = mi; }
+        }
+    }
+    if (wave == 0) {
+        int cntv = 0;
+        for (int e0 = 0; e0 < ne; e0 += 64) {
+            const int e = e0 + lane;
+            cntv += __popcll(__ballot(e < ne && s_idx[s_keep[e < ne ? e / KC : 0]][e % KC] != kNoIdx));
+        }
+        nvalid = cntv;
+    }
+    if (dbg) ts[5] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (wave != 0) return;
+    uint64_t gk = 0ull;
+    int32_t gi = kNoIdx;
+    bool gcut = false;
+    int64_t gcnt = 0;
+    for (int w = 0; w < nw; ++w) {
+        if (s_wci[w] != kNoIdx && (gi == kNoIdx || code_better(s_wck[w], s_wci[w], gk, gi))) { gk = s_wck[w]; gi = s_wci[w]; }
+        gcut = gcut || s_wcut[w] != 0;
+        gcnt += s_wcnt[w];
+    }
+    const int nout = nvalid < K ? nvalid : K;
+    // lists outside the kept K, or entries beyond K, remain: the output is cut
+    const bool left = ntot > nkeep || nvalid > K;
     const int32_t cut_out = (gcut || left) ? 1 : 0;
     if (lane < K) {
         Rec r{};
-        if (mi != kNoIdx) {
+        const uint64_t mc = s_ocode[lane < nout ? lane : 0];
+        const int32_t mi = s_oidx[lane < nout ? lane : 0];
+        const bool ok = lane < nout && !(gi != kNoIdx && code_better(gk, gi, mc, mi));
+        if (ok) {
             const NodeRec &nd = A.nodes[mi - A.node_offset];
-            r.key = mk; r.idx = mi; r.valid = 1;
+            const uint64_t u = (mc >> 63) ? (mc & 0x7fffffffffffffffull) : ~mc;  // inverse of key_code
+            r.key = __longlong_as_double((long long)u); r.idx = mi; r.valid = 1;
             r.a[0] = nd.a[0]; r.a[1] = nd.a[1]; r.a[2] = nd.a[2];
             r.labels = nd.labels; r.price = nd.price;
         } else {
@@ -439,7 +500,12 @@ __global__ __launch_bounds__(64) void k_merge_pod(MergeArgs A) {
         r.pad = lane == 0 ? cut_out : 0;
         A.out_rec[(size_t)b * K + lane] = r;
     }
-    if (lane == 0) A.out_fc[b] = cnt;
+    if (lane == 0) A.out_fc[b] = gcnt;
+    if (dbg && lane == 0) {
+        ts[6] = __builtin_amdgcn_s_memtime();
+        for (int k = 1; k < 7; ++k) atomicAdd((unsigned long long *)&A.dbg[k - 1], (unsigned long long)(ts[k] - ts[k - 1]));
+        atomicAdd((unsigned long long *)&A.dbg[7], 1ull);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -453,6 +519,7 @@ __global__ __launch_bounds__(64) void k_merge_pod(MergeArgs A) {
 // ------------------------------------------------------------------------------------------------
 template <int KIN, int K, bool INPUT_REC, bool FINAL>
 __global__ __launch_bounds__(64) void k_merge(MergeArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     __shared__ double s_key[64 * KIN];
     __shared__ int32_t s_idx[64 * KIN];
     const int lane = threadIdx.x;
@@ -785,6 +852,7 @@ __device__ __forceinline__ int commit_loop(const CommitArgs &A, CommitCtx &cx, i
 
 template <int K, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x;
     const int64_t p0 = *A.plan;
@@ -1068,33 +1136,21 @@ hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const 
 }
 
 namespace {
-template <int KC, int K>
-hipError_t merge_pod_l(const MergeArgs &a, hipStream_t s) {
-    // lists per lane; LPL * KC <= 32 register entries per lane (merge_lists_max)
-    const int lpl = (a.C_in + 63) / 64;
-    if (lpl > merge_lists_max(KC) / 64) return hipErrorInvalidValue;
-    if (lpl <= 1) hipLaunchKernelGGL((k_merge_pod<KC, K, 1>), dim3(a.B), dim3(64), 0, s, a);
-    else if (lpl <= 2) hipLaunchKernelGGL((k_merge_pod<KC, K, 2>), dim3(a.B), dim3(64), 0, s, a);
-    else if constexpr (KC <= 8) {
-        if (lpl <= 4) hipLaunchKernelGGL((k_merge_pod<KC, K, 4>), dim3(a.B), dim3(64), 0, s, a);
-        else if constexpr (KC <= 4) hipLaunchKernelGGL((k_merge_pod<KC, K, 8>), dim3(a.B), dim3(64), 0, s, a);
-    }
-    return hipGetLastError();
-}
 template <int K>
 hipError_t merge_pod_k(int KC, const MergeArgs &a, hipStream_t s) {
     switch (KC) {
-        case 2: return merge_pod_l<2, K>(a, s);
-        case 4: return merge_pod_l<4, K>(a, s);
-        case 8: return merge_pod_l<8, K>(a, s);
-        case 16: return merge_pod_l<16, K>(a, s);
+        case 2: hipLaunchKernelGGL((k_merge_pod<2, K>), dim3(a.B), dim3(kMergeThreads), 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_merge_pod<4, K>), dim3(a.B), dim3(kMergeThreads), 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_merge_pod<8, K>), dim3(a.B), dim3(kMergeThreads), 0, s, a); break;
+        case 16: hipLaunchKernelGGL((k_merge_pod<16, K>), dim3(a.B), dim3(kMergeThreads), 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
 }
 }  // namespace
 
 hipError_t launch_merge_pod(int KC, int K, const MergeArgs &a, hipStream_t s) {
-    if (a.C_in > merge_lists_max(KC) || KC > K) return hipErrorInvalidValue;
+    if (a.C_in > kMergeThreads || KC > K) return hipErrorInvalidValue;
     switch (K) {
         case 4: return merge_pod_k<4>(KC, a, s);
         case 8: return merge_pod_k<8>(KC, a, s);
