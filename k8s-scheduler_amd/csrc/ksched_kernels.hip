@@ -358,6 +358,8 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
     __shared__ uint64_t s_ccode[W * K];             // surviving heads
     __shared__ int32_t s_cidx[W * K], s_clist[W * K];
     __shared__ int32_t s_keep[K];                   // list of global head rank g
+    __shared__ uint64_t s_ecode[K * KC];            // the kept lists' entries
+    __shared__ int32_t s_eidx[K * KC];
     __shared__ uint64_t s_ocode[K];
     __shared__ int32_t s_oidx[K];
     __shared__ uint64_t s_wck[W];
@@ -390,6 +392,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
     }
 #pragma unroll
     for (int q = 0; q < KC; ++q) { s_code[tid][q] = code[q]; s_idx[tid][q] = idx[q]; }
+    if (tid < W * K) { s_ccode[tid] = 0ull; s_cidx[tid] = kNoIdx; }  // empty survivor slots never rank
     if (dbg) { asm volatile("" ::"v"(code[0]), "v"(cnt)); ts[1] = __builtin_amdgcn_s_memtime(); }
     // wave partials: best cutoff (last entry of a full list), count, cut flag
     {
@@ -431,39 +434,39 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
             const uint64_t mc = s_ccode[tid];
             const int32_t mi = s_cidx[tid];
             int g = 0;
-            for (int w2 = 0; w2 < nw; ++w2) {
-                const int nv2 = s_wnv[w2] < K ? s_wnv[w2] : K;
-#pragma unroll 8
-                for (int p2 = 0; p2 < K; ++p2)
-                    g += (p2 < nv2 && code_better(s_ccode[w2 * K + p2], s_cidx[w2 * K + p2], mc, mi)) ? 1 : 0;
-            }
+#pragma unroll 16
+            for (int c = 0; c < W * K; ++c) g += code_better(s_ccode[c], s_cidx[c], mc, mi) ? 1 : 0;
             if (g < K) s_keep[g] = s_clist[tid];
         }
     }
     if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
     __syncthreads();
-    // 3. rank the kept lists' entries against each other
+    // 3. gather the kept lists' entries (empty slots never rank), then rank them against each other
     const int nkeep = ntot < K ? ntot : K;
     const int ne = nkeep * KC;
+    if (tid < K * KC) {
+        const bool in = tid < ne;
+        const int l = in ? s_keep[tid / KC] : 0;
+        s_ecode[tid] = in ? s_code[l][tid % KC] : 0ull;
+        s_eidx[tid] = in ? s_idx[l][tid % KC] : kNoIdx;
+    }
+    __syncthreads();
     int nvalid = 0;
     if (tid < ne) {
-        const int l = s_keep[tid / KC], q = tid % KC;
-        const uint64_t mc = s_code[l][q];
-        const int32_t mi = s_idx[l][q];
+        const uint64_t mc = s_ecode[tid];
+        const int32_t mi = s_eidx[tid];
         if (mi != kNoIdx) {
             int r = 0;
-            for (int e = 0; e < ne; ++e) {
-                const int l2 = s_keep[e / KC], q2 = e % KC;
-                r += code_better(s_code[l2][q2], s_idx[l2][q2], mc, mi) ? 1 : 0;
-            }
+#pragma unroll 16
+            for (int e = 0; e < K * KC; ++e) r += code_better(s_ecode[e], s_eidx[e], mc, mi) ? 1 : 0;
             if (r < K) { s_ocode[r] = mc; s_oidx[r] = mi; }
         }
     }
     if (wave == 0) {
         int cntv = 0;
-        for (int e0 = 0; e0 < ne; e0 += 64) {
+        for (int e0 = 0; e0 < K * KC; e0 += 64) {
             const int e = e0 + lane;
-            cntv += __popcll(__ballot(e < ne && s_idx[s_keep[e < ne ? e / KC : 0]][e % KC] != kNoIdx));
+            cntv += __popcll(__ballot(e < K * KC && s_eidx[e < K * KC ? e : 0] != kNoIdx));
         }
         nvalid = cntv;
     }
