@@ -25,6 +25,20 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-leve
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
 BYTES_PER_PAIR = 24          # node alloc cpu/mem/pods int64 re-read per pod (sequential semantics)
 FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-score pair
+# PMC summary of the same workload (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json")
+
+
+def pmc_traffic(kernel, config, batch):
+    """HBM-side bytes per launch of `kernel` from the committed PMC passes, when they were taken on
+    this workload (c4, the same batch); else None."""
+    if config != "c4" or batch != 64 or not os.path.exists(PMC_SUMMARY):
+        return None, None
+    with open(PMC_SUMMARY) as f:
+        k = json.load(f)["kernels"].get(kernel)
+    if not k or "fabric_bytes_per_launch" not in k:
+        return None, None
+    return k["fabric_bytes_per_launch"], k.get("valu_issue_frac")
 
 
 def parse():
@@ -139,6 +153,7 @@ def main():
     score_avg_ms = fam_ms[0] / max(fam_n[0], 1)
     score_pairs_per_launch = score_pairs / max(fam_n[0], 1)
     achieved_gbs = score_pairs_per_launch * BYTES_PER_PAIR / (score_avg_ms * 1e-3) / 1e9 if score_avg_ms > 0 else 0.0
+    traffic, valu_frac = pmc_traffic(names[0], args.config, int(eng.opts.batch) or 8 * args.topk)
     fam_share = {names[f]: (fam_ms[f] / max(fam_n[f], 1)) for f in range(4)}
     placed = int(st["placed"])
     out = {
@@ -171,7 +186,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_c4_b64.json)",
+            "valu_issue_frac_pmc": valu_frac,
             "algorithmic_bytes_per_pair": BYTES_PER_PAIR,
             "pairs_per_launch": score_pairs_per_launch,
             "avg_launch_ms": score_avg_ms,
