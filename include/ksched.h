@@ -115,6 +115,20 @@ int ksched_load_nodes(ksched_ctx *ctx, int64_t n, const int64_t *alloc_cpu, cons
  * or to undo a bind that failed (anchor/schedule.go:200-237).  node_idx is local to this rank. */
 int ksched_apply_delta(ksched_ctx *ctx, int64_t k, const int32_t *node_idx, const int64_t *d_cpu,
                        const int64_t *d_mem, const int64_t *d_pods);
+/* FailedScheduling diagnostics (anchor/predicate.go:127-157): evaluates the predicate of ONE pod
+ * against the current (local) node state and reports, per node, the first failing check in the
+ * reference's order -- the "fit failure on node (%s): Insufficient CPU|Memory|Pod" lines of the
+ * FailedScheduling event -- then the build-defined label check.  out_counts[KSCHED_REASON_*] counts
+ * nodes per outcome (out_counts[KSCHED_REASON_FIT] == the pod's feasible count); out_reason (n_local
+ * bytes, may be NULL) receives each node's code.  Multi-rank: counts cover this rank's shard. */
+#define KSCHED_REASON_FIT 0
+#define KSCHED_REASON_CPU 1     /* "Insufficient CPU"    anchor/predicate.go:134-138 */
+#define KSCHED_REASON_MEMORY 2  /* "Insufficient Memory" anchor/predicate.go:139-143 */
+#define KSCHED_REASON_POD 3     /* "Insufficient Pod"    anchor/predicate.go:144-148 */
+#define KSCHED_REASON_LABELS 4  /* label selector not satisfied (build extension) */
+#define KSCHED_NUM_REASONS 5
+int ksched_explain(ksched_ctx *ctx, int64_t req_cpu, int64_t req_mem, int64_t req_pods, uint64_t selector,
+                   int64_t out_counts[KSCHED_NUM_REASONS], uint8_t *out_reason);
 /* Copies the current (local) node state back to the host. */
 int ksched_read_nodes(ksched_ctx *ctx, int64_t n, int64_t *alloc_cpu, int64_t *alloc_mem, int64_t *alloc_pods);
 /* Device-side snapshot / restore of the node state (bench: identical start state every step). */

@@ -633,6 +633,31 @@ int ksched_apply_delta(ksched_ctx *c, int64_t k, const int32_t *idx, const int64
     return KSCHED_OK;
 }
 
+int ksched_explain(ksched_ctx *c, int64_t rc, int64_t rm, int64_t rp, uint64_t sel, int64_t out_counts[KSCHED_NUM_REASONS],
+                   uint8_t *out_reason) {
+    if (!c) return KSCHED_E_INVALID;
+    if (c->n_local < 0) return fail(c, KSCHED_E_STATE, "explain before load_nodes");
+    if (!out_counts) return fail(c, KSCHED_E_INVALID, "explain: out_counts is NULL");
+    static_assert(KSCHED_NUM_REASONS == kNumReasons, "reason codes");
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t n = c->n_local;
+    unsigned long long *d_cnt = nullptr;
+    HIPCHK(c, hipMalloc(&d_cnt, KSCHED_NUM_REASONS * sizeof(unsigned long long) + (size_t)(out_reason ? n : 0)));
+    uint8_t *d_reason = out_reason ? (uint8_t *)(d_cnt + KSCHED_NUM_REASONS) : nullptr;
+    unsigned long long h[KSCHED_NUM_REASONS] = {};
+    hipError_t e = hipMemsetAsync(d_cnt, 0, KSCHED_NUM_REASONS * sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess)
+        e = launch_explain(c->d_nodes, n, rc, rm, rp, sel, c->o.use_labels != 0, d_reason, d_cnt, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(h, d_cnt, sizeof(h), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_reason && n > 0) e = hipMemcpy(out_reason, d_reason, (size_t)n, hipMemcpyDeviceToHost);
+    hipFree(d_cnt);
+    if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("explain: ") + hipGetErrorString(e));
+    for (int k = 0; k < KSCHED_NUM_REASONS; ++k) out_counts[k] = (int64_t)h[k];
+    return KSCHED_OK;
+}
+
 int ksched_read_nodes(ksched_ctx *c, int64_t n, int64_t *ac, int64_t *am, int64_t *ap) {
     if (!c) return KSCHED_E_INVALID;
     if (c->n_local < 0) return fail(c, KSCHED_E_STATE, "read_nodes before load_nodes");

@@ -201,6 +201,9 @@ hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const 
 constexpr int kSpcThreads = 512;  // speculative commit: wave 0 guesses and checks, 8 waves evaluate
 hipError_t launch_commit_spc(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
 hipError_t launch_commit_lp(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
+constexpr int kNumReasons = 5;  // fit, Insufficient CPU, Insufficient Memory, Insufficient Pod, labels
+hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
+                          bool use_labels, uint8_t *reason, unsigned long long *counts, hipStream_t s);
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
 hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s);

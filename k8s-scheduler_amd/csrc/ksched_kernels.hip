@@ -999,6 +999,27 @@ __global__ void k_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_
     }
 }
 
+// FailedScheduling reasons of one pod against the current node state (anchor/predicate.go:134-148,
+// the failures list of :157): per node the FIRST failing check in the reference's order -- CPU,
+// Memory, Pod -- then the build-defined label check; 0 = fits.  Lane = node, coalesced u8 stores,
+// per-wave ballot counts folded with one vector atomic per reason per wave.
+__global__ void k_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
+                          int use_labels, uint8_t *reason, unsigned long long *counts) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int r = -1;
+    if (j < n) {
+        const NodeRec &nd = nodes[j];
+        r = nd.a[0] < rc ? 1 : nd.a[1] < rm ? 2 : nd.a[2] < rp ? 3 : (use_labels && (nd.labels & sel) != sel) ? 4 : 0;
+        if (reason) reason[j] = (uint8_t)r;
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kNumReasons; ++k) {
+        const unsigned long long m = __ballot(r == k);
+        if (lane == 0 && m) atomicAdd(counts + k, (unsigned long long)__popcll(m));
+    }
+}
+
 __global__ void k_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -1170,6 +1191,14 @@ hipError_t launch_commit(int K, int prio, int dom, bool lab, bool f53, const Com
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s) {
     hipLaunchKernelGGL(k_apply_delta, dim3(1), dim3(64), 0, s, nodes, n, k, idx, d);
+    return hipGetLastError();
+}
+
+hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
+                          bool use_labels, uint8_t *reason, unsigned long long *counts, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_explain, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n, rc, rm, rp, sel,
+                       (int)use_labels, reason, counts);
     return hipGetLastError();
 }
 

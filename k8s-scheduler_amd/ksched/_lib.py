@@ -25,6 +25,11 @@ NO_POSITIVE_SCORE = -2
 MODE_EXACT, MODE_BATCHED, MODE_AUTO = 0, 1, 2
 PRIORITY_RESOURCE, PRIORITY_BEST_PRICE = 0, 1
 DOMAIN_ALL, DOMAIN_FEASIBLE = 0, 1
+REASON_FIT, REASON_CPU, REASON_MEMORY, REASON_POD, REASON_LABELS = 0, 1, 2, 3, 4
+NUM_REASONS = 5
+# the reference's per-node failure text (anchor/predicate.go:135,140,145)
+REASON_TEXT = {REASON_CPU: "Insufficient CPU", REASON_MEMORY: "Insufficient Memory", REASON_POD: "Insufficient Pod",
+               REASON_LABELS: "node labels do not match the pod's selector"}
 
 _ERRNAMES = {E_INVALID: "E_INVALID", E_DEVICE: "E_DEVICE", E_PARSE: "E_PARSE", E_STATE: "E_STATE",
              E_NOMEM: "E_NOMEM", E_UNKNOWN_NODE: "E_UNKNOWN_NODE"}
@@ -72,6 +77,7 @@ SIGNATURES = [
     ("ksched_set_comm", C.c_int, [CTX, C.c_char_p]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
+    ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),
     ("ksched_read_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P]),
     ("ksched_save_state", C.c_int, [CTX]),
     ("ksched_restore_state", C.c_int, [CTX]),

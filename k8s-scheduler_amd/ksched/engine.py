@@ -92,6 +92,15 @@ class Engine:
         self._chk(L.lib().ksched_apply_delta(self._ctx, ix.shape[0], L.ptr(ix, C.c_int32), L.ptr(dc, C.c_int64),
                                              L.ptr(dm, C.c_int64), L.ptr(dp, C.c_int64)), "apply_delta")
 
+    def explain(self, req_cpu: int, req_mem: int, req_pods: int, selector: int = 0, per_node: bool = True):
+        """Predicate outcome of ONE pod against the current node state (anchor/predicate.go:127-157).
+        Returns (counts int64[NUM_REASONS], reasons uint8[n] | None)."""
+        cnt = np.zeros(L.NUM_REASONS, np.int64)
+        rs = np.empty(max(self.n, 0), np.uint8) if per_node else None
+        self._chk(L.lib().ksched_explain(self._ctx, int(req_cpu), int(req_mem), int(req_pods), int(selector),
+                                         L.ptr(cnt, C.c_int64), L.ptr(rs, C.c_uint8)), "explain")
+        return cnt, rs
+
     def read_nodes(self):
         ac = np.empty(self.n, np.int64); am = np.empty(self.n, np.int64); ap = np.empty(self.n, np.int64)
         self._chk(L.lib().ksched_read_nodes(self._ctx, self.n, L.ptr(ac, C.c_int64), L.ptr(am, C.c_int64),

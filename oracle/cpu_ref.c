@@ -416,6 +416,51 @@ int or_schedule(const or_opts *o, int64_t n, int64_t *ac, int64_t *am, int64_t *
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* FailedScheduling reasons: the failures list of predicate() (anchor/predicate.go:127-157)     */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Per node, the FIRST failing check in the reference's order: CPU (predicate.go:134-138), Memory
+ * (:139-143), Pod (:144-148); then the build-defined label check; 0 = the node is appended to the
+ * feasible list (:149).  reason (n, may be NULL); counts[5] = nodes per code. */
+int or_node_reasons(const or_opts *o, int64_t n, const int64_t *ac, const int64_t *am, const int64_t *ap,
+                    const uint64_t *labels, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
+                    uint8_t *reason, int64_t *counts)
+{
+    int64_t j;
+    int k, use_labels = o->use_labels && labels;
+    for (k = 0; k < 5; k++) counts[k] = 0;
+    for (j = 0; j < n; j++) {
+        int r;
+        if (ac[j] < rc) r = 1;
+        else if (am[j] < rm) r = 2;
+        else if (ap[j] < rp) r = 3;
+        else if (use_labels && (labels[j] & sel) != sel) r = 4;
+        else r = 0;
+        if (reason) reason[j] = (uint8_t)r;
+        counts[r]++;
+    }
+    return OR_OK;
+}
+
+/* or_schedule with, for every pod, the reason counts of its predicate at its turn (counts: p*5).
+ * The FailedScheduling event of a NO_FIT pod lists its nodes with codes 1..3 (predicate.go:157). */
+int or_schedule_reasons(const or_opts *o, int64_t n, int64_t *ac, int64_t *am, int64_t *ap,
+                        const uint64_t *labels, const float *price,
+                        int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
+                        int32_t *out_idx, double *out_score, int32_t *out_feas, int64_t *counts)
+{
+    int64_t i;
+    for (i = 0; i < p; i++) {
+        int r;
+        or_node_reasons(o, n, ac, am, ap, labels, rc[i], rm[i], rp[i], sel ? sel[i] : 0, NULL, counts + 5 * i);
+        r = or_schedule(o, n, ac, am, ap, labels, price, 1, rc + i, rm + i, rp + i, sel ? sel + i : NULL,
+                        out_idx + i, out_score + i, out_feas + i, 1);
+        if (r != OR_OK) return r;
+    }
+    return OR_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Batched restatement: speculative top-K at a batch-start snapshot + ordered commit with the   */
 /* touched-node re-score.  Must equal or_schedule bit-for-bit; it is the CPU model of the GPU   */
 /* batched mode (Batched commit) and of its node-sharded multi-GPU form.             */

@@ -93,6 +93,41 @@ def schedule(cl, nthreads: int = 1, n_pods=None):
     return oi, os_, of, (ac, am, ap)
 
 
+def node_reasons(cl, state, rc, rm, rp, sel=0):
+    """Per-node first failing check of one pod against `state` = (cpu, mem, pods) arrays
+    (anchor/predicate.go:134-148).  Returns (counts int64[5], reason uint8[n])."""
+    ac, am, ap = (np.ascontiguousarray(x, dtype=np.int64) for x in state)
+    lab = None if cl.labels is None else np.ascontiguousarray(cl.labels, dtype=np.uint64)
+    reason = np.empty(ac.shape[0], np.uint8)
+    counts = np.zeros(5, np.int64)
+    o = _opts(cl.priority, cl.domain, cl.use_labels)
+    lib().or_node_reasons(C.byref(o), C.c_int64(ac.shape[0]), _p(ac, C.c_int64), _p(am, C.c_int64), _p(ap, C.c_int64),
+                          _p(lab, C.c_uint64), C.c_int64(int(rc)), C.c_int64(int(rm)), C.c_int64(int(rp)),
+                          C.c_uint64(int(sel)), _p(reason, C.c_uint8), _p(counts, C.c_int64))
+    return counts, reason
+
+
+def schedule_reasons(cl, n_pods=None):
+    """Sequential schedule plus every pod's reason counts at its turn.  Returns
+    (idx, score, feasible, counts int64[P, 5], final state)."""
+    ac, am, ap = (np.ascontiguousarray(x, dtype=np.int64).copy() for x in (cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))
+    p = cl.n_pods if n_pods is None else int(n_pods)
+    rc, rm, rp = (np.ascontiguousarray(x[:p], dtype=np.int64) for x in (cl.req_cpu, cl.req_mem, cl.req_pods))
+    lab = None if cl.labels is None else np.ascontiguousarray(cl.labels, dtype=np.uint64)
+    sel = None if cl.selector is None else np.ascontiguousarray(cl.selector[:p], dtype=np.uint64)
+    pr = None if cl.price is None else np.ascontiguousarray(cl.price, dtype=np.float32)
+    oi = np.empty(p, np.int32); os_ = np.empty(p, np.float64); of = np.empty(p, np.int32)
+    counts = np.zeros((p, 5), np.int64)
+    o = _opts(cl.priority, cl.domain, cl.use_labels)
+    r = lib().or_schedule_reasons(C.byref(o), C.c_int64(ac.shape[0]), _p(ac, C.c_int64), _p(am, C.c_int64),
+                                  _p(ap, C.c_int64), _p(lab, C.c_uint64), _p(pr, C.c_float), C.c_int64(p),
+                                  _p(rc, C.c_int64), _p(rm, C.c_int64), _p(rp, C.c_int64), _p(sel, C.c_uint64),
+                                  _p(oi, C.c_int32), _p(os_, C.c_double), _p(of, C.c_int32), _p(counts, C.c_int64))
+    if r != 0:
+        raise RuntimeError(f"or_schedule_reasons failed: {r}")
+    return oi, os_, of, counts, (ac, am, ap)
+
+
 def schedule_batched(cl, K: int, B: int, n_pods=None):
     ac, am, ap = (np.ascontiguousarray(x, dtype=np.int64).copy() for x in (cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))
     p = cl.n_pods if n_pods is None else int(n_pods)
