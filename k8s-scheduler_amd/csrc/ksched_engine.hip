@@ -241,7 +241,12 @@ int enqueue_batched(ksched_ctx *c) {
     if (impl != KSCHED_COMMIT_SEQUENTIAL && pl.B > 64) impl = KSCHED_COMMIT_SEQUENTIAL;
     const bool lp_commit = impl == KSCHED_COMMIT_LANE_PER_POD;
     const bool spc_commit = impl == KSCHED_COMMIT_SPECULATIVE;
-    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2, sM = one_stream ? c->stream : c->stream3;
+    // merge and commit share stream C by default: the hand-off merge(b) -> commit(b) is then an
+    // in-queue dependency (~2 us) instead of a cross-queue event wait (~12 us, tools/trace_gaps.py);
+    // KSCHED_MC_SPLIT=1 restores a separate merge stream.
+    const bool mc_split = env_int("KSCHED_MC_SPLIT", 0) != 0;
+    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
+    hipStream_t sM = one_stream ? c->stream : (mc_split ? c->stream3 : c->stream2);
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -270,7 +275,7 @@ int enqueue_batched(ksched_ctx *c) {
     if (!one_stream) {  // streams M and C start after the initialisation above
         HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));
         HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
-        HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
+        if (sM != sC) HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
     }
     int64_t resolved = 0, b = 0, last_resolved_b = -1;
     double avg_progress = std::max(1.0, pl.B * 0.75);
@@ -329,7 +334,7 @@ int enqueue_batched(ksched_ctx *c) {
                 fc0 = ma.out_fc;
                 HIPCHK(c, ev_end(c, tm, 3, e0, 0, sM));
             }
-            if (!one_stream) {
+            if (sM != sC) {
                 HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sM));
                 HIPCHK(c, hipStreamWaitEvent(sC, c->ev_lists[b % kRing], 0));
             }
