@@ -247,6 +247,11 @@ int enqueue_batched(ksched_ctx *c) {
     const bool mc_split = env_int("KSCHED_MC_SPLIT", 0) != 0;
     hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
     hipStream_t sM = one_stream ? c->stream : (mc_split ? c->stream3 : c->stream2);
+    // score(b) -> merge(b) is a cross-queue event wait (~12 us).  KSCHED_DEVICE_HANDOFF=1 makes the
+    // merge poll Ctl::scored on the device instead: measured c4 +4%, but c5 -19% (the 64 early-resident
+    // merge workgroups take slots the score grid needs: score 82 -> 110 us), so it is off by default.
+    const bool dev_handoff = !one_stream && env_int("KSCHED_DEVICE_HANDOFF", 0) != 0;
+    unsigned long long scored_target = 0;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -299,11 +304,13 @@ int enqueue_batched(ksched_ctx *c) {
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part) + (size_t)(b % 2) * part_elems * pl.KC;
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt) + (size_t)(b % 2) * part_elems;
             sa.patch = xbuf(b - 2);
+            sa.done = dev_handoff ? &ctl->scored : nullptr;
+            scored_target += (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
             HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
             // M: merge b while stream S scores b+1 (the lists' part buffers alternate)
-            if (!one_stream) {
+            if (!one_stream && !dev_handoff) {
                 HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
                 HIPCHK(c, hipStreamWaitEvent(sM, c->ev_scored[b % kRing], 0));
             }
@@ -314,6 +321,9 @@ int enqueue_batched(ksched_ctx *c) {
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
                 ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
                 ma.dbg = c->d_mdbg;
+                ma.wait_ctr = dev_handoff ? &ctl->scored : nullptr;
+                ma.wait_target = scored_target;
+                ma.err = c->d_err;
                 ma.out_rec = reinterpret_cast<Rec *>(lists_base);
                 ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
                 HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sM));
@@ -795,6 +805,10 @@ int ksched_sync(ksched_ctx *c) {
     }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e == 2) {
+        hipMemset(c->d_err, 0, sizeof(int32_t));
+        return fail(c, KSCHED_E_DEVICE, "batched mode: the merge's wait for the score workgroups timed out");
+    }
     if (e) return fail(c, KSCHED_E_DEVICE, "exact mode: cross-workgroup exchange timed out (workgroups not co-resident?)");
     return KSCHED_OK;
 }

@@ -59,6 +59,7 @@ struct alignas(8) Ctl {
     int64_t resync;     // 1: a batch truncated; the next plan restarts at cursor
     int64_t stats[5];   // batches committed, truncated, placed, skipped, pairs scored
     int64_t plan[kPlanRing];
+    unsigned long long scored;  // score workgroups finished this call (device hand-off to the merge)
 };
 
 struct PodArgs {
@@ -97,6 +98,7 @@ struct ScoreArgs {
     Cand *part;        // [B][workgroups][KC]
     int64_t *part_cnt; // [B][workgroups]
     const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
+    unsigned long long *done;  // Ctl::scored (null: the merge waits on a stream event instead)
 };
 
 struct MergeArgs {
@@ -117,6 +119,9 @@ struct MergeArgs {
     const int64_t *cursor;
     int64_t P;
     int32_t B;
+    const unsigned long long *wait_ctr;  // k_merge_pod: poll until *wait_ctr >= wait_target (null: no wait)
+    unsigned long long wait_target;
+    int32_t *err;                        // device error word (2 = the wait timed out)
 };
 
 struct CommitArgs {

@@ -221,7 +221,7 @@ __device__ __forceinline__ void list_insert_ordered(double (&key)[KC], int32_t (
 }
 
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
+__device__ __forceinline__ void score_topk_body(const ScoreArgs &A) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     double *s_key = reinterpret_cast<double *>(smem);                                   // [W/2][KC][64]
     int32_t *s_idx = reinterpret_cast<int32_t *>(smem + (size_t)(kScoreWaves / 2) * KC * 64 * 8);
@@ -333,6 +333,44 @@ __global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
     }
 }
 
+// Device-side hand-off score(b) -> merge(b) (MI355X_MICROARCH "valid forms", producer side): every
+// storing wave drains its stores, the workgroup meets, lane 0 writes back the XCD L2 (agent release),
+// drains that, then adds to the monotone counter Ctl::scored.  The merge polls the counter instead of
+// waiting on a cross-queue event.
+__device__ __forceinline__ void signal_scored(unsigned long long *done) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int KC, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
+    score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
+    if (A.done) signal_scored(A.done);
+}
+
+// Consumer side: one relaxed (sc1) poll with s_sleep, one agent acquire, drain, workgroup barrier.  A
+// wall-clock timeout (2 s) sets the device error word instead of spinning forever.
+__device__ __forceinline__ void wait_scored(const unsigned long long *ctr, unsigned long long target, int32_t *err) {
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > 200000000ull) {
+                if (err) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Merge of one pod's workgroup lists (C_in <= 512 lists of KC entries, cut when full) into its K-entry
 // Rec list: one 512-thread workgroup per pod, thread = list.  Selection by RANK, every compare
@@ -374,6 +412,7 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
     if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
     const int64_t p0 = *A.cursor;
     if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // workgroup-uniform
+    if (A.wait_ctr) wait_scored(A.wait_ctr, A.wait_target, A.err);
     const bool has = tid < A.C_in;
     uint64_t code[KC];
     int32_t idx[KC];
@@ -972,6 +1011,7 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     if (threadIdx.x != 0) return;
     ctl->cursor = 0; ctl->spec_next = 0; ctl->resync = 0;
     for (int i = 0; i < 5; ++i) ctl->stats[i] = 0;
+    ctl->scored = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;
     ctl->plan[0] = P > 0 ? 0 : -1;
     ctl->plan[1] = B < P ? B : -1;
