@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "libksched.so")
+# KSCHED_LIB: an alternative in-tree build of the same ABI (A/B measurements of kernel variants)
+LIB_PATH = os.environ.get("KSCHED_LIB") or os.path.join(PKG_ROOT, "libksched.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "ksched.h")
 
 OK = 0
