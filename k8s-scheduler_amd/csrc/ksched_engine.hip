@@ -252,6 +252,11 @@ int enqueue_batched(ksched_ctx *c) {
     // merge workgroups take slots the score grid needs: score 82 -> 110 us), so it is off by default.
     const bool dev_handoff = !one_stream && env_int("KSCHED_DEVICE_HANDOFF", 0) != 0;
     unsigned long long scored_target = 0;
+    // Fused merge (KSCHED_FUSE_MERGE=1; single rank, KC 4 / K 16, one pod group, >= B score workgroups):
+    // parity-green but measured slower (c4 7.5e10 vs 1.05e11: score+merge 75 us vs 47+15, and the
+    // commit co-running with it 71 us vs 37), so the separate merge kernel stays the default.
+    const bool fuse = !one_stream && !dev_handoff && !c->comm && pl.KC == 4 && pl.K == 16 && pl.pod_groups == 1 &&
+                      pl.n_chunks / kScoreWaves >= pl.B && !c->d_mdbg && env_int("KSCHED_FUSE_MERGE", 0) != 0;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -304,31 +309,38 @@ int enqueue_batched(ksched_ctx *c) {
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part) + (size_t)(b % 2) * part_elems * pl.KC;
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt) + (size_t)(b % 2) * part_elems;
             sa.patch = xbuf(b - 2);
-            sa.done = dev_handoff ? &ctl->scored : nullptr;
-            scored_target += (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
+            const unsigned long long g_launch = (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
+            sa.done = (dev_handoff || fuse) ? &ctl->scored : nullptr;
+            sa.fuse_merge = fuse ? 1 : 0;
+            sa.g_total = (int32_t)g_launch;
+            sa.done_base = scored_target;
+            scored_target += g_launch;
+            MergeArgs ma{};
+            ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
+            ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
+            ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
+            ma.dbg = c->d_mdbg;
+            ma.wait_ctr = dev_handoff ? &ctl->scored : nullptr;
+            ma.wait_target = scored_target;
+            ma.err = c->d_err;
+            ma.out_rec = reinterpret_cast<Rec *>(lists_base);
+            ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
-            HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
+            HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, ma, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
             // M: merge b while stream S scores b+1 (the lists' part buffers alternate)
-            if (!one_stream && !dev_handoff) {
+            if (fuse) {  // score(b) produced the merged lists: commit(b) waits for it directly
                 HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
-                HIPCHK(c, hipStreamWaitEvent(sM, c->ev_scored[b % kRing], 0));
-            }
-            HIPCHK(c, ev_begin(c, tm, &e0, sM));
-            {
-                MergeArgs ma{};
-                ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
-                ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
-                ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
-                ma.dbg = c->d_mdbg;
-                ma.wait_ctr = dev_handoff ? &ctl->scored : nullptr;
-                ma.wait_target = scored_target;
-                ma.err = c->d_err;
-                ma.out_rec = reinterpret_cast<Rec *>(lists_base);
-                ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
+                HIPCHK(c, hipStreamWaitEvent(sC, c->ev_scored[b % kRing], 0));
+            } else {
+                if (!one_stream && !dev_handoff) {
+                    HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
+                    HIPCHK(c, hipStreamWaitEvent(sM, c->ev_scored[b % kRing], 0));
+                }
+                HIPCHK(c, ev_begin(c, tm, &e0, sM));
                 HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sM));
+                HIPCHK(c, ev_end(c, tm, 1, e0, 0, sM));
             }
-            HIPCHK(c, ev_end(c, tm, 1, e0, 0, sM));
             const Rec *lists = reinterpret_cast<const Rec *>(lists_base);
             const int64_t *fc0 = reinterpret_cast<const int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
             if (c->comm) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
@@ -344,7 +356,7 @@ int enqueue_batched(ksched_ctx *c) {
                 fc0 = ma.out_fc;
                 HIPCHK(c, ev_end(c, tm, 3, e0, 0, sM));
             }
-            if (sM != sC) {
+            if (sM != sC && !fuse) {
                 HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sM));
                 HIPCHK(c, hipStreamWaitEvent(sC, c->ev_lists[b % kRing], 0));
             }

@@ -99,6 +99,10 @@ struct ScoreArgs {
     int64_t *part_cnt; // [B][workgroups]
     const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
     unsigned long long *done;  // Ctl::scored (null: the merge waits on a stream event instead)
+    // fused merge (KC 4, K 16, single rank): the last B workgroups to finish merge one pod each
+    int32_t fuse_merge;
+    int32_t g_total;                 // workgroups of this launch
+    unsigned long long done_base;    // Ctl::scored before this launch
 };
 
 struct MergeArgs {
@@ -196,7 +200,7 @@ constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
 hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s);
 hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool fast53, const ExactArgs &a, int block,
                         bool cooperative, hipStream_t s);
-hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, const MergeArgs &m, int pod_groups,
                              hipStream_t s);
 // one workgroup per pod: the score kernel's workgroup lists -> the pod's K-entry Rec list (C_in <= 256)
 hipError_t launch_merge_pod(int KC, int K, const MergeArgs &a, hipStream_t s);
@@ -220,7 +224,7 @@ hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, doub
 constexpr int kExactBlock = 256;
 
 // score kernel geometry: 4 waves per workgroup, 2 workgroups per CU at the default grid
-constexpr int kScoreWaves = 4;
+constexpr int kScoreWaves = 8;
 constexpr int kMergeThreads = 512;  // merge: one workgroup per pod, lane = one workgroup list (<= 512)
 constexpr int kScoreThreads = kScoreWaves * 64;
 constexpr size_t score_lds_bytes(int KC) { return (size_t)(kScoreWaves / 2) * KC * 64 * 12 + 64 * 4; }

@@ -347,11 +347,6 @@ __device__ __forceinline__ void signal_scored(unsigned long long *done) {
     }
 }
 
-template <int KC, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A) {
-    score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
-    if (A.done) signal_scored(A.done);
-}
 
 // Consumer side: one relaxed (sc1) poll with s_sleep, one agent acquire, drain, workgroup barrier.  A
 // wall-clock timeout (2 s) sets the device error word instead of spinning forever.
@@ -388,7 +383,7 @@ __device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb
 }
 
 template <int KC, int K>
-__global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
+__device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     constexpr int W = kMergeThreads / 64;
     __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
@@ -406,7 +401,6 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int b = blockIdx.x;
     const bool dbg = A.dbg != nullptr;
     uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
@@ -547,6 +541,39 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
         ts[6] = __builtin_amdgcn_s_memtime();
         for (int k = 1; k < 7; ++k) atomicAdd((unsigned long long *)&A.dbg[k - 1], (unsigned long long)(ts[k] - ts[k - 1]));
         atomicAdd((unsigned long long *)&A.dbg[7], 1ull);
+    }
+}
+
+template <int KC, int K>
+__global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
+    merge_pod_body<KC, K>(A, blockIdx.x);
+}
+
+// Score kernel.  FUSE (KC 4, K 16, single rank): every workgroup publishes its lists (release) and
+// takes an arrival number from Ctl::scored; the last B arrivals wait for the rest (at most B - 1
+// workgroups, all already dispatched or dispatchable: no early-resident consumers) and merge one pod
+// each, so no merge kernel and no score -> merge queue hand-off exist.
+template <int KC, int PRIO, int DOM, bool LAB, bool F53, bool FUSE>
+__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A, MergeArgs M) {
+    score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
+    if constexpr (FUSE) {
+        static_assert(kScoreThreads == kMergeThreads, "fused merge runs one pod per score workgroup");
+        __shared__ int s_arr;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            s_arr = (int)(__hip_atomic_fetch_add(A.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - A.done_base);
+        }
+        __syncthreads();
+        const int first = A.g_total - A.B;
+        const int arr = s_arr;
+        if (arr < first) return;
+        wait_scored(A.done, A.done_base + (unsigned long long)A.g_total, M.err);
+        merge_pod_body<4, 16>(M, arr - first);
+    } else {
+        if (A.done) signal_scored(A.done);
     }
 }
 
@@ -1096,28 +1123,32 @@ hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStrea
     }
 }
 
-template <int KC, int PRIO, int DOM, bool LAB, bool F53>
-hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
+template <int KC, int PRIO, int DOM, bool LAB, bool F53, bool FUSE>
+hipError_t score_one(const ScoreArgs &a, const MergeArgs &m, int pod_groups, hipStream_t s) {
     const size_t lds = score_lds_bytes(KC);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_score_topk<KC, PRIO, DOM, LAB, F53>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_score_topk<KC, PRIO, DOM, LAB, F53, FUSE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     dim3 grid((unsigned)(a.n_chunks / kScoreWaves), pod_groups);
-    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53>), grid, dim3(kScoreThreads), lds, s, a);
+    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53, FUSE>), grid, dim3(kScoreThreads), lds, s, a, m);
     return hipGetLastError();
 }
 
 template <int PRIO, int DOM, bool LAB, bool F53>
-hipError_t score_k(int KC, const ScoreArgs &a, int pg, hipStream_t s) {
+hipError_t score_k(int KC, const ScoreArgs &a, const MergeArgs &m, int pg, hipStream_t s) {
+    if (a.fuse_merge) {
+        if (KC != 4 || pg != 1) return hipErrorInvalidValue;
+        return score_one<4, PRIO, DOM, LAB, F53, true>(a, m, pg, s);
+    }
     switch (KC) {
-        case 2: return score_one<2, PRIO, DOM, LAB, F53>(a, pg, s);
-        case 4: return score_one<4, PRIO, DOM, LAB, F53>(a, pg, s);
-        case 8: return score_one<8, PRIO, DOM, LAB, F53>(a, pg, s);
-        case 16: return score_one<16, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 2: return score_one<2, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
+        case 4: return score_one<4, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
+        case 8: return score_one<8, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
+        case 16: return score_one<16, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1185,9 +1216,9 @@ hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool f53, const Ex
     KSCHED_DISPATCH(prio, dom, lab, f53, (exact_npt<P_, D_, L_, F_>(npt, a, block, coop, s)));
 }
 
-hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, const MergeArgs &m, int pod_groups,
                              hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(KC, a, pod_groups, s)));
+    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(KC, a, m, pod_groups, s)));
 }
 
 hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s) {
