@@ -265,3 +265,16 @@ def test_sharded_engine_helper_world1(gpu_available, oracle_mod):
     st = eng.read_nodes()
     eng.close()
     assert_same((oi, os_, of, st), oracle_mod.schedule(cl), "sharded-helper")
+
+
+@pytest.mark.parametrize("env", ["KSCHED_FUSE_MERGE", "KSCHED_DEVICE_HANDOFF", "KSCHED_MC_SPLIT", "KSCHED_ONE_STREAM"])
+def test_pipeline_variants_parity(gpu_available, oracle_mod, env, monkeypatch):
+    """The measured-and-rejected pipeline layouts stay bit-exact: fused
+    score+merge (last-arrival workgroups merge), device-side score->merge hand-off, separate merge
+    stream, single stream.  Each is selected by its environment switch at enqueue time."""
+    from ksched import MODE_BATCHED, cluster
+    monkeypatch.setenv(env, "1")
+    for name, nn, pp in (("c3", 30000, 2000), ("c5", 40000, 1500)):
+        cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+        want = oracle_mod.schedule(cl, nthreads=8)
+        assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=64), want, f"{name}/{env}")
