@@ -62,6 +62,7 @@ struct SpcSmem {
     double *pbk;      // [16 waves][64 pods] partial best key over the wave's guessed columns
     int64_t *pbx;     // [16 waves][64 pods] (slot << 32) | node of that best
     int32_t *ctl;     // [0] round start c, [1] window end, [2] stop
+    int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none)
 };
 
 __device__ __forceinline__ uint32_t spc_hash(int32_t idx) {
@@ -147,12 +148,13 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
         m.gq = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
+        m.own = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
         m.D = reinterpret_cast<int8_t *>(p);
     }
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
 
     // ---- prologue (all waves) ----
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
     for (int e = tid; e < 64 * K; e += kSpcThreads) {
@@ -243,32 +245,38 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
         if (dbg) t_mark = __builtin_amdgcn_s_memtime();
         if (wave == 0) {
             const int cend = (c + W < nb) ? c + W : nb;
-            int ng = 0;
-            // taken bitmap, one word per lane (lane w holds positions 32w .. 32w+31): confirmed touches,
-            // plus this round's guesses as they are made
-            uint32_t tkw = m.tkc[lane];
+            // Guesses by fixpoint iteration, lane = pod: g_i = the first list entry of pod i that is neither
+            // confirmed-taken nor proposed by a pod < i (own[pos] < i) in the previous iteration.  Pod i's
+            // proposal is final once those of all pods < i are, so the fixpoint is reached after at most
+            // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
+            // the rule (99 %), it is reached after two.
             const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
-            const int32_t *HPl = m.HP + lane * 64;    // lane q: list entry q of every pod
-            int pos_n = lane < K && c < cend ? HPl[c] : kSpcInvalid;
-            for (int i = c; i < cend; ++i) {
-                const int pos = pos_n;
-                pos_n = lane < K && i + 1 < cend ? HPl[i + 1] : kSpcInvalid;  // prefetch the next pod's entries
-                int32_t q = -1, sl = -1, h = kSpcInvalid, g = -2;
-                if ((fitm >> i) & 1) {
-                    const uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((pos >> 5) << 2, (int)tkw);
-                    const uint64_t fm = __ballot(lane < K && !((w >> (pos & 31)) & 1u));
-                    if (fm) {
-                        q = (int32_t)__builtin_ctzll(fm);
-                        h = __builtin_amdgcn_readlane(pos, q);
-                        tkw |= (lane == (h >> 5)) ? (1u << (h & 31)) : 0u;
-                        sl = nT + ng;
-                        ++ng;
-                        g = 0;
-                    } else {
-                        g = -1;
+            const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
+            int32_t pq = -1, ph = kSpcInvalid;  // current proposal (list position, table position)
+            for (int it = 0;; ++it) {
+                int32_t nq = -1, nh = kSpcInvalid;
+                if (act) {
+                    for (int qq = 0; qq < K; ++qq) {
+                        const int pos = m.HP[qq * 64 + lane];
+                        if (pos == kSpcInvalid) break;  // valid entries form a prefix
+                        const bool tk = (m.tkc[pos >> 5] >> (pos & 31)) & 1u;
+                        if (!tk && m.own[pos] >= lane) { nq = qq; nh = pos; break; }
                     }
                 }
-                if (lane == i) { my_g = g; my_q = q; my_s = sl; my_h = h; }
+                const bool changed = __ballot(act && nq != pq) != 0;
+                if (act && pq >= 0) m.own[ph] = 64;
+                lds_order();
+                pq = nq; ph = nh;
+                if (!changed && it > 0) break;
+                if (act && pq >= 0) atomicMin(&m.own[ph], lane);
+                lds_order();
+            }
+            const uint64_t gm = __ballot(act && pq >= 0);
+            if (lane >= c && lane < cend) {
+                my_g = act ? (pq >= 0 ? 0 : -1) : -2;
+                my_q = pq;
+                my_h = act && pq >= 0 ? ph : kSpcInvalid;
+                my_s = act && pq >= 0 ? nT + __popcll(gm & ((1ull << lane) - 1ull)) : -1;
             }
             const bool in = lane >= c && lane < cend;
             if (in && my_g == 0) my_g = m.LI[my_q * 64 + lane];  // the guessed node
@@ -557,7 +565,8 @@ namespace {
 template <int K>
 constexpr size_t spc_lds_bytes() {
     return (size_t)64 * kSpcRow * 8 + (size_t)kSpcWaves * 64 * 16 + (size_t)K * 64 * 12 + kSpcSlots * sizeof(SpcSlot) +
-           (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 + kSpcSlots * 4 + 5 * 64 * 4 + 16 + 64 * 64;
+           (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 + kSpcSlots * 4 + 5 * 64 * 4 + 16 + (size_t)kSpcHash * 4 +
+           64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
 
