@@ -152,6 +152,16 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
         m.D = reinterpret_cast<int8_t *>(p);
     }
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
+    // every wave: lane = pod j of the batch (lanes >= nb carry a zero request and are never read).
+    // Issued before the prologue so these global loads overlap the list loads instead of following
+    // them behind a barrier.
+    const bool pj = lane < nb;
+    const int64_t rc = pj ? A.pods.rc[p0 + lane] : 0;
+    const int64_t rm = pj ? A.pods.rm[p0 + lane] : 0;
+    const int64_t rp = pj ? A.pods.rp[p0 + lane] : 0;
+    const uint64_t sel = (LAB && pj) ? A.pods.sel[p0 + lane] : 0;
+    const int64_t fc0v = (wave == 0 && pj) ? A.fc0[lane] : 0;
+    const int cut0 = (wave == 0 && pj) ? A.lists[(size_t)lane * K].pad : 0;
 
     // ---- prologue (all waves) ----
     for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
@@ -182,12 +192,6 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
     }
     __syncthreads();
 
-    // every wave: lane = pod j of the batch (lanes >= nb carry a zero request and are never read)
-    const bool pj = lane < nb;
-    const int64_t rc = pj ? A.pods.rc[p0 + lane] : 0;
-    const int64_t rm = pj ? A.pods.rm[p0 + lane] : 0;
-    const int64_t rp = pj ? A.pods.rp[p0 + lane] : 0;
-    const uint64_t sel = (LAB && pj) ? A.pods.sel[p0 + lane] : 0;
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
     double *Srow = m.S + (size_t)lane * kSpcRow;
@@ -225,8 +229,8 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
     int nT = nin, done = nb, W = 64;
     int64_t placed = 0, nrounds = 0, nfail = 0;
     if (wave == 0) {
-        fcc = pj ? (int32_t)(A.fc0[lane] + m.dfacc[lane]) : 0;
-        cut = pj ? A.lists[(size_t)lane * K].pad : 0;
+        fcc = pj ? (int32_t)(fc0v + m.dfacc[lane]) : 0;
+        cut = cut0;
 #pragma unroll
         for (int q = 0; q < K; ++q) cv += m.LI[q * 64 + lane] != kNoIdx;  // valid entries form a prefix
         for (int w = 0; w < kSpcWaves; ++w) {
