@@ -54,14 +54,38 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-baseline-s", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--check", action="store_true", help="verify a prefix against the CPU oracle")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the (untimed) prefix check of the timed run's results against the CPU oracle")
+    ap.add_argument("--check-pods", type=int, default=5000)
     return ap.parse_args()
+
+
+def host_cpu():
+    """(threads this process may use, CPU model name) -- the host side of the cpu_baseline line."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():  # the GPU box grants a 16-thread CPU share
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return max(1, n), model
 
 
 def cpu_baseline(cl, budget_s):
     """The oracle's sequential C restatement (single thread, -O2 -ffp-contract=off), timed on this host
     on a bounded prefix of the same workload: the first p pods at full node count (per-pod cost is
-    constant in the pod index)."""
+    constant in the pod index).  Then the same restatement node-parallel on every thread this process
+    may use (OpenMP, one barrier per pod)."""
+    nthr, model = host_cpu()
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.lib()
@@ -77,17 +101,16 @@ def cpu_baseline(cl, budget_s):
     rate = p * cl.n_nodes / t
     mt = None
     try:
-        nthr = os.cpu_count() or 1
-        nthr = min(nthr, 16)
-        pm = max(16, min(cl.n_pods, int(p * 2)))
+        pm = max(16, min(cl.n_pods, int(p * max(2, nthr // 2))))
         t0 = time.perf_counter()
         O.schedule(cl, nthreads=nthr, n_pods=pm)
         tm = time.perf_counter() - t0
-        mt = dict(value=pm * cl.n_nodes / tm, unit="pod-node evals/s", cores=nthr, kind="port",
-                  sample=f"first {pm} pods of {cl.name} at {cl.n_nodes} nodes, OpenMP node-parallel, one barrier per pod")
+        mt = dict(value=pm * cl.n_nodes / tm, unit="pod-node evals/s", cores=nthr, kind="port", cpu_model=model,
+                  sample=f"first {pm} pods of {cl.name} at {cl.n_nodes} nodes, OpenMP node-parallel on {nthr} threads "
+                         f"(all this process may use), one barrier per pod ({tm:.1f} s)")
     except Exception:
         pass
-    return dict(value=rate, unit="pod-node evals/s", cores=1, kind="port",
+    return dict(value=rate, unit="pod-node evals/s", cores=1, kind="port", cpu_model=model,
                 sample=f"first {p} pods of {cl.name} at full {cl.n_nodes} nodes, sequential commit, 1 thread "
                        f"({t:.1f} s; Go reference unbuildable here: no Go toolchain)"), mt
 
@@ -113,14 +136,18 @@ def main():
     if world > 1 and mode == MODE_EXACT:
         mode = MODE_BATCHED
     eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=local, mode=mode, topk=args.topk,
-                                        batch=args.batch, timing=True)
+                                        batch=args.batch, timing=False)
     eng.save_state()
     eng.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
 
     def step():
+        """One schedulePods pass: restore the initial node state on device, resolve every pending pod
+        in order, wait, and bring the assignments back to the host (the wall ends with
+        assignments-on-host)."""
         eng.restore_state()
         eng.run()
         eng.sync()
+        return eng.results()
 
     for _ in range(args.warmup):
         step()
@@ -128,10 +155,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kstats = []
     for _ in range(args.steps):
-        step()
-        kstats.append(eng.stats())
+        res = step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -143,7 +168,14 @@ def main():
     ms = elapsed * 1000.0 / args.steps
     pairs = cl.n_pods * cl.n_nodes
     value = pairs * args.steps / elapsed
-    st = kstats[-1]
+    st_timed = eng.stats()
+    # one more (untimed) pass with sampled per-kernel HIP events on the engine's streams: the
+    # roofline's per-launch durations come from here, not from inside the timed region
+    eng.set_timing(True, 8)
+    step()
+    kstats = [eng.stats()]
+    eng.set_timing(False)
+    st = st_timed
     # dominant kernel family by timed device time (sampled batches)
     names = ["k_exact" if mode == MODE_EXACT else "k_score_topk", "k_merge", "k_commit", "rccl_allgather+merge"]
     fam_ms = [sum(s["kernel_ms"][f] for s in kstats) for f in range(4)]
@@ -202,14 +234,17 @@ def main():
         out["cpu_baseline"] = base
         if mt:
             out["cpu_baseline_mt"] = mt
-    if args.check and rank == 0 and world == 1:
+    if not args.no_check and rank == 0:
+        # the timed run's own results, prefix against the CPU oracle (pods resolve in order, so the
+        # first k results of the full run are the results of a k-pod run); outside the timed region
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
-        oi, os_, of = eng.results()
-        k = min(cl.n_pods, 2000)
-        wi, ws, wf, _ = O.schedule(cl, nthreads=8, n_pods=k)
+        oi, os_, of = res
+        k = min(cl.n_pods, args.check_pods)
+        wi, ws, wf, _ = O.schedule(cl, nthreads=host_cpu()[0], n_pods=k)
         out["check_prefix_pods"] = k
-        out["check_ok"] = bool(np.array_equal(oi[:k], wi) and np.array_equal(os_[:k].view(np.int64), ws.view(np.int64)))
+        out["check_ok"] = bool(np.array_equal(oi[:k], wi) and np.array_equal(os_[:k].view(np.int64), ws.view(np.int64))
+                               and np.array_equal(of[:k], wf))
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

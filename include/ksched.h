@@ -153,6 +153,9 @@ int ksched_run(ksched_ctx *ctx);                 /* schedules the staged pods; r
 int ksched_sync(ksched_ctx *ctx);                /* waits for the run; fills stats */
 int ksched_download_results(ksched_ctx *ctx, int64_t p, int32_t *out_idx, double *out_score, int32_t *out_feasible);
 int ksched_get_stats(const ksched_ctx *ctx, ksched_stats *out);
+/* Turns the sampled per-kernel HIP-event timing (opts.timing / opts.timing_every) on or off for the
+ * following calls (every = 0: keep the current sampling period). */
+int ksched_set_timing(ksched_ctx *ctx, int32_t timing, int32_t every);
 
 /* Diagnostics: out_native[i] = a[i] / b[i] (hipcc's f64 division) and out_fast[i] = the engine's
  * hoisted-reciprocal division of the same operands, both computed on the device (bit-exactness

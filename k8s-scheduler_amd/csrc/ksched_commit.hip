@@ -291,7 +291,7 @@ __global__ __launch_bounds__(kLpThreads) void k_commit_lp(CommitArgs A) {
             const double wk = kind == 1 ? uki : tk;
             const int32_t wi = kind == 1 ? uii : ti;
             oidx = wi;
-            osc = PRIO == kPrioPrice ? -wk : wk;
+            osc = PRIO == kPrioPrice ? 0.0 - wk : wk;
             ++placed;
             int s;
             int64_t b0, b1, b2;

@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
             const bool conf = lane >= c && lane < f;
             if (conf) {
                 my_idx = kind == 1 ? my_g : (fcj == 0 ? -1 : -2);
-                my_score = kind == 1 ? (PRIO == kPrioPrice ? -uk : uk) : 0.0;
+                my_score = kind == 1 ? (PRIO == kPrioPrice ? 0.0 - uk : uk) : 0.0;
                 my_feas = fcj;
                 if (guessed_commit) atomicOr(&m.tkc[my_h >> 5], 1u << (my_h & 31));
             }
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
                 } else {
                     if (lane == f) {
                         my_idx = kf == 0 ? (fcf == 0 ? -1 : -2) : wi;
-                        my_score = kf == 0 ? 0.0 : (PRIO == kPrioPrice ? -wk : wk);
+                        my_score = kf == 0 ? 0.0 : (PRIO == kPrioPrice ? 0.0 - wk : wk);
                         my_feas = fcf;
                     }
                     if (kf != 0) {

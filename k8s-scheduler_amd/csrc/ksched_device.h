@@ -130,13 +130,18 @@ __device__ __forceinline__ double resource_score_fast(int64_t rc, int64_t rm, in
     return s;
 }
 
+// Best-price key: -price, with +0.0 for both signed zeros (x + 0.0 maps -0 to +0 in round-to-nearest
+// and is not folded under -fno-fast-math): ranked by bit pattern in the merge, a price of -0 must not
+// outrank a price of 0 at a lower node index.
+__host__ __device__ __forceinline__ double price_key(float price) { return -(double)price + 0.0; }
+
 template <int PRIO, int DOM, bool FAST53>
 __device__ __forceinline__ bool pair_key_fast(bool feas, int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,
                                               double rpf, int64_t ac, int64_t am, int64_t ap, double acf,
                                               double amf, double apf, double yc, double ym, double yp, double y3,
                                               float price, double *key) {
     if (PRIO == kPrioPrice) {
-        *key = -(double)price;
+        *key = price_key(price);
         return feas;
     } else {
         if (DOM == kDomFeasible && !feas) return false;
@@ -218,7 +223,7 @@ __device__ __forceinline__ bool pair_key(bool feas, int64_t rc, int64_t rm, int6
                                          double rpf, int64_t ac, int64_t am, int64_t ap, double acf, double amf,
                                          double apf, float price, double *key) {
     if (PRIO == kPrioPrice) {
-        *key = -(double)price;
+        *key = price_key(price);
         return feas;
     } else {
         if (DOM == kDomFeasible && !feas) return false;

@@ -33,6 +33,7 @@ struct ksched_ctx {
     bool has_labels = false, has_price = false;
     uint64_t max_abs_alloc = 0;  // saturating bound on |allocatable| (fast53 check)
     uint64_t sum_abs_req = 0;    // saturating sum of |request| over the staged pods
+    uint64_t snap_max_abs_alloc = 0;  // max_abs_alloc of the save_state snapshot
     NodeRec *d_nodes = nullptr, *d_snap = nullptr;
     int64_t node_cap = 0;
     // pods
@@ -601,7 +602,10 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
     if (c->o.use_labels && n > 0 && !labels) return fail(c, KSCHED_E_INVALID, "load_nodes: use_labels needs labels");
     if (c->o.priority == KSCHED_PRIORITY_BEST_PRICE && n > 0 && !price)
         return fail(c, KSCHED_E_INVALID, "load_nodes: best-price priority needs prices");
-    if (n > 0x7ffffff0LL) return fail(c, KSCHED_E_INVALID, "load_nodes: too many nodes");
+    // node indices are int32 on the device and kNoIdx (INT32_MAX) marks "no candidate": every global
+    // index this rank produces (node_offset + local) must stay below it
+    if (c->o.node_offset < 0 || n > 0x7ffffff0LL || c->o.node_offset + n > 0x7ffffff0LL)
+        return fail(c, KSCHED_E_INVALID, "load_nodes: node_offset + n must stay below 2^31 - 16");
     std::vector<NodeRec> h((size_t)std::max<int64_t>(n, 0));
     uint64_t mx = 0;
     for (int64_t i = 0; i < n; ++i) {
@@ -610,7 +614,7 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
         r.af[0] = r.af[1] = r.af[2] = 0.0;  // derived on the device (k_prep_nodes) with the reciprocals
         r.y[0] = r.y[1] = r.y[2] = 0.0;
         r.labels = labels ? labels[i] : 0;
-        r.price = price ? price[i] : 0.f;
+        r.price = (price && price[i] != 0.f) ? price[i] : 0.f;  // "-0" == "0": canonical +0 (price_key)
         r.pad[0] = r.pad[1] = r.pad[2] = 0;
         mx = std::max(mx, std::max(uabs(ac[i]), std::max(uabs(am[i]), uabs(ap[i]))));
         if (price && !std::isfinite(price[i])) return fail(c, KSCHED_E_INVALID, "load_nodes: non-finite price");
@@ -709,6 +713,7 @@ int ksched_save_state(ksched_ctx *c) {
     if (c->n_local > 0)
         HIPCHK(c, hipMemcpyAsync(c->d_snap, c->d_nodes, (size_t)c->n_local * sizeof(NodeRec), hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->snap_max_abs_alloc = c->max_abs_alloc;
     return KSCHED_OK;
 }
 
@@ -718,6 +723,7 @@ int ksched_restore_state(ksched_ctx *c) {
     HIPCHK(c, hipSetDevice(c->dev));
     if (c->n_local > 0)
         HIPCHK(c, hipMemcpyAsync(c->d_nodes, c->d_snap, (size_t)c->n_local * sizeof(NodeRec), hipMemcpyDeviceToDevice, c->stream));
+    c->max_abs_alloc = c->snap_max_abs_alloc;
     return KSCHED_OK;
 }
 
@@ -794,6 +800,9 @@ int ksched_run(ksched_ctx *c) {
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->running = r == KSCHED_OK;
+    // the call's commits move every allocatable by at most the sum of the staged requests: keep the
+    // FAST53 bound true of the state the NEXT call starts from
+    if (r == KSCHED_OK) c->max_abs_alloc = sat_add(c->max_abs_alloc, c->sum_abs_req);
     return r;
 }
 
@@ -845,6 +854,13 @@ int ksched_download_results(ksched_ctx *c, int64_t p, int32_t *oi, double *os, i
 int ksched_get_stats(const ksched_ctx *c, ksched_stats *out) {
     if (!c || !out) return KSCHED_E_INVALID;
     *out = c->st;
+    return KSCHED_OK;
+}
+
+int ksched_set_timing(ksched_ctx *c, int32_t timing, int32_t every) {
+    if (!c || every < 0) return KSCHED_E_INVALID;
+    c->o.timing = timing ? 1 : 0;
+    if (every > 0) c->o.timing_every = every;
     return KSCHED_OK;
 }
 

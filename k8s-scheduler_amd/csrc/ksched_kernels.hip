@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
             oidx = -2;  // NO_POSITIVE_SCORE (reference: nil node, anchor/priorities.go:55-62)
         } else {
             oidx = gi;
-            osc = PRIO == kPrioPrice ? -gk : gk;
+            osc = PRIO == kPrioPrice ? 0.0 - gk : gk;
 #pragma unroll
             for (int k = 0; k < NPT; ++k) {
                 if (id[k] == gi) {  // commit: used += request, ONE pod (anchor/predicate.go:99-102)
@@ -755,7 +755,7 @@ __device__ __forceinline__ void rescore_touched(const CommitCtx &cx, int64_t rc,
         df += (int64_t)__popcll(__ballot(f1)) - (int64_t)__popcll(__ballot(f0));
         bool c;
         if (PRIO == kPrioPrice) {
-            c = f1 && better(-(double)x.price, x.idx, thk, thi);
+            c = f1 && better(price_key(x.price), x.idx, thk, thi);
         } else {
             bool near1;
             const double hi = resource_score_upper<F53>(rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
@@ -853,7 +853,7 @@ __device__ __forceinline__ bool commit_step(const CommitArgs &A, CommitCtx &cx, 
             oidx = -2;
         } else {
             oidx = wi;
-            osc = PRIO == kPrioPrice ? -wk : wk;
+            osc = PRIO == kPrioPrice ? 0.0 - wk : wk;
             ++cx.placed;
             int slot = ts;
             int writer = 0;

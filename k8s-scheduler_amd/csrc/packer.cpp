@@ -187,7 +187,9 @@ extern "C" int ksched_parse_price(const char *s, float *out) {
     if (!out || !s) return KSCHED_E_INVALID;
     double v;
     if (parse_float32(s, &v) != FloatErr::ok || !std::isfinite(v)) return KSCHED_E_PARSE;
-    *out = (float)v;
+    // "-0" and "0" are the same price: canonical +0 keeps the lowest-index tie rule intact where
+    // keys are ranked by bit pattern (the merge's order-preserving key codes)
+    *out = v == 0.0 ? 0.0f : (float)v;
     return KSCHED_OK;
 }
 

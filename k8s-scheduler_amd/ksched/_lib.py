@@ -88,6 +88,7 @@ SIGNATURES = [
     ("ksched_sync", C.c_int, [CTX]),
     ("ksched_download_results", C.c_int, [CTX, C.c_int64, I32P, F64P, I32P]),
     ("ksched_get_stats", C.c_int, [CTX, C.POINTER(Stats)]),
+    ("ksched_set_timing", C.c_int, [CTX, C.c_int32, C.c_int32]),
     ("ksched_selftest_fastdiv", C.c_int, [CTX, C.c_int64, F64P, F64P, F64P, F64P]),
     ("ksched_parse_cpu", C.c_int, [C.c_char_p, I64P]),
     ("ksched_parse_memory", C.c_int, [C.c_char_p, I64P]),

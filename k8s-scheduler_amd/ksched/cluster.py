@@ -22,6 +22,10 @@ import numpy as np
 DECIMAL_CPU = ("0.1", "0.15", "0.2", "0.25", "0.3", "0.35", "0.4", "0.5", "0.6", "0.7",
                "0.75", "0.8", "0.9", "1.1", "1.2", "1.3", "1.5", "1.7", "2.3", "3.3")
 
+HC_USED_LO, HC_USED_SPAN = 0.97, 0.027  # c5hc node usage (cpu and memory)
+HC_POD_SCALE = 1                        # c5hc pod requests relative to the standard pods
+HC_HOT_EVERY = 100                      # c5hc: one fresh large node per this many nodes
+
 PRIORITY_RESOURCE = 0
 PRIORITY_BEST_PRICE = 1
 DOMAIN_ALL = 0
@@ -95,8 +99,12 @@ CONFIGS = {
     "c3": (50_000, 100_000, PRIORITY_RESOURCE, DOMAIN_ALL, False, "batched"),
     "c4": (100_000, 1_000_000, PRIORITY_RESOURCE, DOMAIN_ALL, False, "batched"),
     "c5": (200_000, 500_000, PRIORITY_RESOURCE, DOMAIN_FEASIBLE, True, "batched"),
+    # c5 made genuinely high-conflict: nodes 97-99.7 % used except one fresh large
+    # node in every 100, so every batch piles onto the same few fresh nodes -- placements re-touch
+    # nodes of the batch, and most batches exhaust some pod's candidate list (truncation + re-score)
+    "c5hc": (200_000, 500_000, PRIORITY_RESOURCE, DOMAIN_FEASIBLE, True, "batched"),
 }
-CONFIG_IDS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5}
+CONFIG_IDS = {"c1": 1, "c2": 2, "c3": 3, "c4": 4, "c5": 5, "c5hc": 6}
 SEED_BASE = 20260915
 
 
@@ -140,13 +148,23 @@ def make_cluster(name: str, seed: Optional[int] = None, n_nodes: Optional[int] =
         cap_cpu = cores * 1000
         cap_mem = cores * rng.choice(np.array([2, 4, 8], dtype=np.int64), size=nn) * (1 << 20)
         cap_pods = rng.choice(np.array([110, 250], dtype=np.int64), size=nn)
-        ucpu = 0.85 + rng.random(nn) * 0.13
-        umem = 0.85 + rng.random(nn) * 0.13
+        lo, span = (0.85, 0.13) if name == "c5" else (HC_USED_LO, HC_USED_SPAN)
+        ucpu = lo + rng.random(nn) * span
+        umem = lo + rng.random(nn) * span
         upod = 0.85 + rng.random(nn) * 0.13
+        if name == "c5hc":  # every HC_HOT_EVERY-th node is a fresh (empty) large node
+            hot = np.arange(nn) % HC_HOT_EVERY == HC_HOT_EVERY - 1
+            cores[hot] = rng.integers(64, 193, size=int(hot.sum()))
+            cap_cpu[hot] = cores[hot] * 1000
+            cap_mem[hot] = cores[hot] * 8 * (1 << 20)
+            ucpu[hot] = umem[hot] = upod[hot] = 0.0
     used_cpu = np.floor(ucpu * cap_cpu).astype(np.int64)
     used_mem = np.floor(umem * cap_mem).astype(np.int64)
     used_pod = np.floor(upod * cap_pods).astype(np.int64)
     cpu, mem, ncont, use_dec, dec_i, cpu_m, mem_mi, zero = _pods_standard(rng, pp)
+    if name == "c5hc":  # large pods: every container's request scaled up
+        cpu, mem, cpu_m, mem_mi = cpu * HC_POD_SCALE, mem * HC_POD_SCALE, cpu_m * HC_POD_SCALE, mem_mi * HC_POD_SCALE
+        use_dec[:] = False
     c = Cluster(name=name,
                 alloc_cpu=cap_cpu - used_cpu, alloc_mem=cap_mem - used_mem, alloc_pods=cap_pods - used_pod,
                 req_cpu=cpu.sum(1), req_mem=mem.sum(1), req_pods=ncont,

@@ -142,6 +142,10 @@ class Engine:
                     pair_evals=s.pair_evals, device_ms=s.device_ms, kernel_ms=list(s.kernel_ms),
                     kernel_launches=list(s.kernel_launches), kernel_pairs=list(s.kernel_pairs))
 
+    def set_timing(self, on: bool, every: int = 0):
+        """Sampled per-kernel HIP-event timing for the following calls (every: one batch in N)."""
+        self._chk(L.lib().ksched_set_timing(self._ctx, int(bool(on)), int(every)), "set_timing")
+
     def schedule(self, req_cpu, req_mem, req_pods, selector=None):
         """schedulePods over the given pending pods (in order).  Returns (idx, score, feasible)."""
         self.upload_pods(req_cpu, req_mem, req_pods, selector)

@@ -321,8 +321,10 @@ class FakeCluster:
 
     def schedule_pods(self, pending: Optional[List[Pod]] = None, selectors=None):
         """schedulePods (anchor/schedule.go:185-197): one engine call resolves every pending pod in order;
-        binds follow in the same order.  Returns a list of (pod, node | Exception)."""
-        pending = [p for p in self.pods if not p.node_name] if pending is None else pending
+        binds follow in the same order.  Returns a list of (pod, node | Exception).  By default the
+        pending set is getUnscheduledPods' (unbound pods annotated for this scheduler,
+        anchor/schedule.go:175-177); pass `pending` to schedule any other list (the watch path)."""
+        pending = self.unscheduled_pods() if pending is None else pending
         rc, rm, rp = pack_pods(pending)
         if selectors is None and self.use_labels:
             selectors = [self.selector_of(p) for p in pending]

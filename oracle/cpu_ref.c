@@ -331,7 +331,7 @@ static inline int pair_key(const or_opts *o, int feas, int64_t rc, int64_t rm, i
 
 static inline double out_score_of(const or_opts *o, double key)
 {
-    return o->priority == OR_PRIORITY_BEST_PRICE ? -key : key;
+    return o->priority == OR_PRIORITY_BEST_PRICE ? 0.0 - key : key; /* the price; both signed zeros give +0 */
 }
 
 /* ------------------------------------------------------------------------------------------ */

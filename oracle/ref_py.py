@@ -189,7 +189,7 @@ def schedule(nodes, pods, priority=0, domain=0, use_labels=False, labels=None, s
             out_i.append(-2); out_s.append(0.0)
             continue
         out_i.append(best)
-        out_s.append(-bkey if priority == 1 else bkey)
+        out_s.append(0.0 - bkey if priority == 1 else bkey)  # the price; "-0" and "0" both give +0
         st[best][0] = _wrap64(st[best][0] - rc)
         st[best][1] = _wrap64(st[best][1] - rm)
         st[best][2] = _wrap64(st[best][2] - 1)

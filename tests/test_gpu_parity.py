@@ -158,7 +158,8 @@ def test_host_mirror_fake_cluster(gpu_available, oracle_mod):
              for i, (nm, conts) in enumerate(cl.bound_pods)]
     pend = [Pod(f"p{i}", [Container(requests=r) for r in conts]) for i, conts in enumerate(cl.pending_pods)]
     fc = FakeCluster(nodes, bound + pend, priority=cl.priority, domain=cl.domain)
-    res = fc.schedule_pods()
+    assert fc.schedule_pods() == []  # none carries the scheduler annotation (anchor/schedule.go:176)
+    res = fc.schedule_pods(pend)
     want = oracle_mod.schedule(cl)
     for (pod, r), wi in zip(res, want[0]):
         if wi >= 0:
@@ -278,3 +279,33 @@ def test_pipeline_variants_parity(gpu_available, oracle_mod, env, monkeypatch):
         cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
         want = oracle_mod.schedule(cl, nthreads=8)
         assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=64), want, f"{name}/{env}")
+
+
+def test_signed_zero_prices_keep_lowest_index(gpu_available, oracle_mod):
+    """Prices 0 and -0 are the same price: the lowest node index must win in every mode, including
+    when the two nodes land in different score workgroups and are ranked by key bits in the merge."""
+    from ksched import cluster
+    n, p = 6000, 400
+    rng = np.random.default_rng(7)
+    price = (1.0 + rng.integers(0, 50, size=n) / 8).astype(np.float32)
+    zeros = [3, 700, 1500, 2999, 4100, 5998]
+    for k, j in enumerate(zeros):
+        price[j] = np.float32(-0.0) if k % 2 else np.float32(0.0)
+    cl = cluster.Cluster(name="signed-zero", alloc_cpu=np.full(n, 4000, np.int64),
+                         alloc_mem=np.full(n, 8 << 20, np.int64), alloc_pods=np.full(n, 110, np.int64),
+                         req_cpu=rng.integers(100, 1500, size=p).astype(np.int64),
+                         req_mem=rng.integers(1, 1 << 20, size=p).astype(np.int64), req_pods=np.ones(p, np.int64),
+                         price=price, priority=cluster.PRIORITY_BEST_PRICE, domain=cluster.DOMAIN_FEASIBLE)
+    want = oracle_mod.schedule(cl)
+    assert want[0][0] == 3 and not np.signbit(want[1][0])
+    for name, mode, kw in modes():
+        assert_same(run_engine(cl, mode, **kw), want, f"signed-zero/{name}")
+
+
+def test_load_nodes_rejects_index_overflow(gpu_available):
+    """Global node indices are int32 with INT32_MAX reserved for "no candidate"."""
+    from ksched import Engine, KschedError
+    one = np.ones(4, np.int64)
+    with Engine(node_offset=(1 << 31) - 18, nodes_global=1 << 31) as e:
+        with pytest.raises(KschedError):
+            e.load_nodes(one, one, one)
