@@ -106,6 +106,17 @@ const char *ksched_last_error(const ksched_ctx *ctx); /* never NULL; "" when no 
 int ksched_get_unique_id(uint8_t out_id[128]);
 int ksched_set_comm(ksched_ctx *ctx, const uint8_t id[128]);
 
+/* In-process rank group: the same node-sharded batched path with R contexts of ONE process on ONE
+ * device (one host thread per context), the per-batch all-gather done by host-coordinated device
+ * copies instead of RCCL (RCCL admits one rank per device).  It runs the multi-rank code on a single
+ * GPU (a test vehicle, one host round trip per batch); contexts set opts.rank / nranks / node_offset /
+ * nodes_global as for ksched_set_comm, call ksched_set_group instead of it, and must run the same
+ * schedule calls concurrently. */
+typedef struct ksched_group ksched_group;
+int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out);
+int ksched_group_destroy(ksched_group *g); /* after every context using it is destroyed */
+int ksched_set_group(ksched_ctx *ctx, ksched_group *g);
+
 /* ---- node state (allocatable = capacity - used, anchor/predicate.go:56-67) ---- */
 /* Loads this rank's n nodes (node order = nodeList.Items order).  labels / price may be NULL
  * unless the options need them.  Prices must be finite. */
@@ -129,6 +140,17 @@ int ksched_apply_delta(ksched_ctx *ctx, int64_t k, const int32_t *node_idx, cons
 #define KSCHED_NUM_REASONS 5
 int ksched_explain(ksched_ctx *ctx, int64_t req_cpu, int64_t req_mem, int64_t req_pods, uint64_t selector,
                    int64_t out_counts[KSCHED_NUM_REASONS], uint8_t *out_reason);
+/* The same diagnostics for EVERY pod of the last schedule call (ksched_schedule / ksched_run) that
+ * ended KSCHED_NO_FIT, each against the node state it saw at its turn -- the state after the
+ * placements of all pods before it (anchor/schedule.go:185-197 re-reads the cluster per pod) -- with
+ * no host replay: out_counts[i * KSCHED_NUM_REASONS + r] for pod i (rows of the other pods are
+ * zero); *out_nofit (may be NULL) = their number.  Valid only while the last call's placements are
+ * the last change to the node state (KSCHED_E_STATE after load_nodes / apply_delta / restore_state /
+ * upload_pods).  Multi-rank: counts cover this rank's shard (sum them over ranks). */
+int ksched_explain_batch(ksched_ctx *ctx, int64_t p, int64_t *out_counts, int64_t *out_nofit);
+/* Per-node reasons of pod `pod` of the last schedule call at its turn: the "fit failure on node"
+ * lines of its FailedScheduling event (out_reason: n_local bytes, may be NULL). */
+int ksched_explain_pod(ksched_ctx *ctx, int64_t pod, int64_t out_counts[KSCHED_NUM_REASONS], uint8_t *out_reason);
 /* Copies the current (local) node state back to the host. */
 int ksched_read_nodes(ksched_ctx *ctx, int64_t n, int64_t *alloc_cpu, int64_t *alloc_mem, int64_t *alloc_pods);
 /* Device-side snapshot / restore of the node state (bench: identical start state every step). */

@@ -34,6 +34,18 @@ struct alignas(16) NodeRec {
     uint32_t pad[3];
 };
 static_assert(sizeof(NodeRec) == 96, "NodeRec layout");
+// The same rows seen through the constant address space: wave-uniform reads become scalar loads.
+typedef __attribute__((address_space(4))) NodeRec NodeRecC;
+
+__device__ __forceinline__ NodeRec load_row(const NodeRecC *p) {
+    NodeRec r;
+    r.a[0] = p->a[0]; r.a[1] = p->a[1]; r.a[2] = p->a[2];
+    r.labels = p->labels;
+    r.af[0] = p->af[0]; r.af[1] = p->af[1]; r.af[2] = p->af[2];
+    r.y[0] = p->y[0]; r.y[1] = p->y[1]; r.y[2] = p->y[2];
+    r.price = p->price;
+    return r;
+}
 
 // One candidate of a partial top-K list (score kernels -> merge kernels).
 struct alignas(16) Cand {

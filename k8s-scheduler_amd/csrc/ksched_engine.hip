@@ -9,7 +9,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -20,6 +23,41 @@
 #include "ksched_kernels.h"
 
 using namespace ksched;
+
+// In-process rank group (include/ksched.h).  The all-gather is host-coordinated and synchronous:
+// every rank waits for its own send block, the ranks meet, each copies every rank's block into its
+// receive buffer (device-to-device on the shared device) and waits for the copies, and the ranks meet
+// again before any send block can be rewritten.  No kernel ever waits on another rank's work, so the
+// ranks' streams may share hardware queues (GPU_MAX_HW_QUEUES) without deadlock.  Slower than RCCL by
+// a host round trip per batch: a test vehicle for the multi-rank code, not a bench path.
+struct ksched_group {
+    int nranks = 0, dev = 0;
+    int64_t block_bytes = 0;
+    std::vector<const char *> send;  // each rank's send block of the current exchange
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0, acc = 0, result = 0;
+    uint64_t gen = 0;
+};
+
+namespace {
+// all R ranks meet; returns the minimum of their values (false: a rank never arrived)
+bool group_min(ksched_group *g, int v, int *out) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    const uint64_t gen = g->gen;
+    g->acc = g->arrived == 0 ? v : std::min(g->acc, v);
+    if (++g->arrived == g->nranks) {
+        g->result = g->acc;
+        g->arrived = 0;
+        ++g->gen;
+        g->cv.notify_all();
+    } else if (!g->cv.wait_for(lk, std::chrono::seconds(30), [&] { return g->gen != gen; })) {
+        return false;
+    }
+    *out = g->result;
+    return true;
+}
+}  // namespace
 
 struct ksched_ctx {
     ksched_opts o{};
@@ -61,6 +99,7 @@ struct ksched_ctx {
     int64_t slots_cap = 0;
     // multi-GPU
     ncclComm_t comm = nullptr;
+    ksched_group *group = nullptr;  // in-process rank group (instead of comm)
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool running = false;
@@ -71,6 +110,12 @@ struct ksched_ctx {
     size_t ev_used = 0;
     ksched_stats st{};
     int64_t run_batches = 0;
+    // batch FailedScheduling diagnostics (ksched_explain_batch / ksched_explain_pod)
+    bool explain_valid = false;  // the last state change was the last schedule call's placements
+    void *d_xws = nullptr;
+    size_t xws_bytes = 0;
+    void *d_xbuf = nullptr;      // counts + NO_FIT pod list, or one pod's state + counts
+    size_t xbuf_bytes = 0;
 };
 
 namespace {
@@ -195,7 +240,11 @@ BatchPlan plan_batch(const ksched_ctx *c) {
 int decide_fast53(ksched_ctx *c) {
     int flag = sat_add(c->max_abs_alloc, c->sum_abs_req) < (1ull << 52) ? 1 : 0;
     if (env_int("KSCHED_NO_FAST53", 0)) flag = 0;
-    if (c->comm) {
+    if (c->group) {
+        int mn = flag;
+        if (!group_min(c->group, flag, &mn)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer never called run");
+        flag = mn;
+    } else if (c->comm) {
         int32_t *d = c->d_err;  // scratch word (zeroed again before use by exact mode)
         HIPCHK(c, hipMemcpyAsync(d, &flag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
         NCCLCHK(c, ncclAllReduce(d, d, 1, ncclInt32, ncclMin, c->comm, c->stream));
@@ -256,7 +305,7 @@ int enqueue_batched(ksched_ctx *c) {
     // Fused merge (KSCHED_FUSE_MERGE=1; single rank, KC 4 / K 16, one pod group, >= B score workgroups):
     // parity-green but measured slower (c4 7.5e10 vs 1.05e11: score+merge 75 us vs 47+15, and the
     // commit co-running with it 71 us vs 37), so the separate merge kernel stays the default.
-    const bool fuse = !one_stream && !dev_handoff && !c->comm && pl.KC == 4 && pl.K == 16 && pl.pod_groups == 1 &&
+    const bool fuse = !one_stream && !dev_handoff && !c->comm && !c->group && pl.KC == 4 && pl.K == 16 && pl.pod_groups == 1 &&
                       pl.n_chunks / kScoreWaves >= pl.B && !c->d_mdbg && env_int("KSCHED_FUSE_MERGE", 0) != 0;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
@@ -344,9 +393,23 @@ int enqueue_batched(ksched_ctx *c) {
             }
             const Rec *lists = reinterpret_cast<const Rec *>(lists_base);
             const int64_t *fc0 = reinterpret_cast<const int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
-            if (c->comm) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
+            if (c->comm || c->group) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
                 HIPCHK(c, ev_begin(c, tm, &e0, sM));
-                NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sM));
+                if (c->comm) {
+                    NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sM));
+                } else {
+                    ksched_group *g = c->group;
+                    int dummy;
+                    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sM));
+                    HIPCHK(c, hipEventSynchronize(c->ev_pipe[0]));  // my block is final
+                    g->send[(size_t)c->o.rank] = lists_base;
+                    if (!group_min(g, 0, &dummy)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer stopped exchanging");
+                    for (int q = 0; q < R; ++q)
+                        HIPCHK(c, hipMemcpyAsync(ws + pl.off_recv + (size_t)q * pl.send_bytes, g->send[(size_t)q],
+                                                 pl.send_bytes, hipMemcpyDeviceToDevice, sM));
+                    HIPCHK(c, hipStreamSynchronize(sM));
+                    if (!group_min(g, 0, &dummy)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer stopped exchanging");
+                }
                 MergeArgs ma{};
                 ma.in = ws + pl.off_recv; ma.rank_stride = (int64_t)pl.send_bytes; ma.C_in = R; ma.C_out = 1;
                 ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
@@ -567,6 +630,7 @@ int ksched_destroy(ksched_ctx *c) {
     }
     for (int i = 0; i < 2; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
+    hipFree(c->d_xws); hipFree(c->d_xbuf);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
     if (c->stream3) hipStreamDestroy(c->stream3);
@@ -592,6 +656,44 @@ int ksched_set_comm(ksched_ctx *c, const uint8_t id[128]) {
     std::memcpy(&uid, id, 128);
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     NCCLCHK(c, ncclCommInitRank(&c->comm, c->o.nranks, uid, c->o.rank));
+    return KSCHED_OK;
+}
+
+int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out) {
+    if (!out || nranks < 1 || nranks > 1024) return KSCHED_E_INVALID;
+    *out = nullptr;
+    ksched_group *g = new (std::nothrow) ksched_group();
+    if (!g) return KSCHED_E_NOMEM;
+    g->nranks = nranks;
+    g->send.assign((size_t)nranks, nullptr);
+    if (device >= 0) {
+        if (hipSetDevice(device) != hipSuccess) { delete g; return KSCHED_E_DEVICE; }
+        g->dev = device;
+    } else if (hipGetDevice(&g->dev) != hipSuccess) {
+        delete g;
+        return KSCHED_E_DEVICE;
+    }
+    *out = g;
+    return KSCHED_OK;
+}
+
+int ksched_group_destroy(ksched_group *g) {
+    delete g;
+    return KSCHED_OK;
+}
+
+int ksched_set_group(ksched_ctx *c, ksched_group *g) {
+    if (!c || !g) return KSCHED_E_INVALID;
+    if (g->nranks != c->o.nranks) return fail(c, KSCHED_E_INVALID, "set_group: group size != opts.nranks");
+    if (c->dev != g->dev) return fail(c, KSCHED_E_INVALID, "set_group: the group's contexts must share its device");
+    if (c->comm) return fail(c, KSCHED_E_STATE, "set_group: context already has an RCCL communicator");
+    const int64_t bytes = (int64_t)c->B * c->K * (int64_t)sizeof(Rec) + (int64_t)c->B * (int64_t)sizeof(int64_t);
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->block_bytes == 0) g->block_bytes = bytes;
+        else if (g->block_bytes != bytes) return fail(c, KSCHED_E_INVALID, "set_group: ranks disagree on batch / topk");
+    }
+    c->group = g;
     return KSCHED_OK;
 }
 
@@ -628,6 +730,7 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->max_abs_alloc = mx;
     c->n_local = n;
+    c->explain_valid = false;
     c->n_global = c->o.nranks > 1 ? c->o.nodes_global : (c->o.nodes_global > 0 ? c->o.nodes_global : n);
     if (c->n_global < c->o.node_offset + n) return fail(c, KSCHED_E_INVALID, "load_nodes: nodes_global too small");
     c->has_labels = labels != nullptr;
@@ -656,6 +759,7 @@ int ksched_apply_delta(ksched_ctx *c, int64_t k, const int32_t *idx, const int64
     if (hipMalloc(&d_d, (size_t)k * 24) != hipSuccess) { hipFree(d_idx); return fail(c, KSCHED_E_DEVICE, "apply_delta: alloc"); }
     hipError_t e = hipMemcpy(d_idx, idx, (size_t)k * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_d, d.data(), (size_t)k * 24, hipMemcpyHostToDevice);
+    c->explain_valid = false;
     if (e == hipSuccess) e = launch_apply_delta(c->d_nodes, c->n_local, k, d_idx, d_d, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     hipFree(d_idx);
@@ -686,6 +790,89 @@ int ksched_explain(ksched_ctx *c, int64_t rc, int64_t rm, int64_t rp, uint64_t s
     hipFree(d_cnt);
     if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("explain: ") + hipGetErrorString(e));
     for (int k = 0; k < KSCHED_NUM_REASONS; ++k) out_counts[k] = (int64_t)h[k];
+    return KSCHED_OK;
+}
+
+namespace {
+ExplainArgs explain_args(ksched_ctx *c) {
+    ExplainArgs a{};
+    a.idx = c->d_oidx; a.p = c->p;
+    a.rc = c->d_rc; a.rm = c->d_rm; a.rp = c->d_rp; a.sel = c->d_sel;
+    a.nodes = c->d_nodes; a.n_local = c->n_local; a.node_lo = c->o.node_offset;
+    a.use_labels = c->o.use_labels != 0;
+    return a;
+}
+
+hipError_t grow_bytes(void **p, size_t *cap, size_t need) {
+    if (*p && *cap >= need) return hipSuccess;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, std::max<size_t>(need, 256));
+    if (e == hipSuccess) *cap = std::max<size_t>(need, 256);
+    return e;
+}
+}  // namespace
+
+int ksched_explain_batch(ksched_ctx *c, int64_t p, int64_t *out_counts, int64_t *out_nofit) {
+    if (!c) return KSCHED_E_INVALID;
+    if (!out_counts && p > 0) return fail(c, KSCHED_E_INVALID, "explain_batch: out_counts is NULL");
+    if (p != c->p) return fail(c, KSCHED_E_INVALID, "explain_batch: p differs from the last schedule call");
+    if (!c->explain_valid) return fail(c, KSCHED_E_STATE, "explain_batch: the node state changed since the last schedule call");
+    if (p >= 0x7fffffff) return fail(c, KSCHED_E_INVALID, "explain_batch: too many pods");
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::memset(out_counts, 0, (size_t)p * KSCHED_NUM_REASONS * sizeof(int64_t));
+    if (out_nofit) *out_nofit = 0;
+    if (p == 0 || c->n_local == 0) return KSCHED_OK;
+    const size_t cnt_bytes = (size_t)p * kNumReasons * sizeof(unsigned long long);
+    HIPCHK(c, grow_bytes(&c->d_xbuf, &c->xbuf_bytes, cnt_bytes + (size_t)p * sizeof(int32_t)));
+    unsigned long long *d_cnt = static_cast<unsigned long long *>(c->d_xbuf);
+    int32_t *d_fpod = reinterpret_cast<int32_t *>(static_cast<char *>(c->d_xbuf) + cnt_bytes);
+    HIPCHK(c, hipMemsetAsync(d_cnt, 0, cnt_bytes, c->stream));
+    ExplainArgs a = explain_args(c);
+    int64_t nf = 0;
+    a.fpod_out = d_fpod;
+    a.n_nofit = &nf;
+    HIPCHK(c, explain_batch(a, &c->d_xws, &c->xws_bytes, d_cnt, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (nf == 0) return KSCHED_OK;
+    std::vector<unsigned long long> h((size_t)nf * kNumReasons);
+    std::vector<int32_t> fp((size_t)nf);
+    HIPCHK(c, hipMemcpy(h.data(), d_cnt, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(fp.data(), d_fpod, fp.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+    for (int64_t f = 0; f < nf; ++f)
+        for (int r = 0; r < kNumReasons; ++r)
+            out_counts[(size_t)fp[(size_t)f] * kNumReasons + r] = (int64_t)h[(size_t)f * kNumReasons + r];
+    if (out_nofit) *out_nofit = nf;
+    return KSCHED_OK;
+}
+
+int ksched_explain_pod(ksched_ctx *c, int64_t pod, int64_t out_counts[KSCHED_NUM_REASONS], uint8_t *out_reason) {
+    if (!c) return KSCHED_E_INVALID;
+    if (!out_counts) return fail(c, KSCHED_E_INVALID, "explain_pod: out_counts is NULL");
+    if (pod < 0 || pod >= c->p) return fail(c, KSCHED_E_INVALID, "explain_pod: pod out of range");
+    if (!c->explain_valid) return fail(c, KSCHED_E_STATE, "explain_pod: the node state changed since the last schedule call");
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t n = c->n_local;
+    ExplainArgs a = explain_args(c);
+    HIPCHK(c, hipMemcpy(&a.q_rc, c->d_rc + pod, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&a.q_rm, c->d_rm + pod, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&a.q_rp, c->d_rp + pod, 8, hipMemcpyDeviceToHost));
+    if (c->o.use_labels) HIPCHK(c, hipMemcpy(&a.q_sel, c->d_sel + pod, 8, hipMemcpyDeviceToHost));
+    const size_t st_bytes = (size_t)3 * std::max<int64_t>(n, 1) * sizeof(int64_t);
+    HIPCHK(c, grow_bytes(&c->d_xbuf, &c->xbuf_bytes, st_bytes + 64 + (size_t)std::max<int64_t>(n, 1)));
+    int64_t *d_state = static_cast<int64_t *>(c->d_xbuf);
+    unsigned long long *d_cnt = reinterpret_cast<unsigned long long *>(static_cast<char *>(c->d_xbuf) + st_bytes);
+    uint8_t *d_reason = reinterpret_cast<uint8_t *>(d_cnt + 8);
+    HIPCHK(c, hipMemsetAsync(d_cnt, 0, kNumReasons * sizeof(unsigned long long), c->stream));
+    HIPCHK(c, explain_pod_at(a, pod, d_state, out_reason ? d_reason : nullptr, d_cnt, c->stream));
+    unsigned long long h[kNumReasons] = {};
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h, d_cnt, sizeof(h), hipMemcpyDeviceToHost));
+    if (out_reason && n > 0) HIPCHK(c, hipMemcpy(out_reason, d_reason, (size_t)n, hipMemcpyDeviceToHost));
+    for (int r = 0; r < kNumReasons; ++r) out_counts[r] = (int64_t)h[r];
     return KSCHED_OK;
 }
 
@@ -724,6 +911,7 @@ int ksched_restore_state(ksched_ctx *c) {
     if (c->n_local > 0)
         HIPCHK(c, hipMemcpyAsync(c->d_nodes, c->d_snap, (size_t)c->n_local * sizeof(NodeRec), hipMemcpyDeviceToDevice, c->stream));
     c->max_abs_alloc = c->snap_max_abs_alloc;
+    c->explain_valid = false;
     return KSCHED_OK;
 }
 
@@ -759,6 +947,7 @@ int ksched_upload_pods(ksched_ctx *c, int64_t p, const int64_t *rc, const int64_
     for (int64_t i = 0; i < p; ++i) sum = sat_add(sum, sat_add(uabs(rc[i]), sat_add(uabs(rm[i]), uabs(rp[i]) + 1)));
     c->sum_abs_req = sum;
     c->p = p;
+    c->explain_valid = false;
     return KSCHED_OK;
 }
 
@@ -783,7 +972,8 @@ int ksched_selftest_fastdiv(ksched_ctx *c, int64_t n, const double *a, const dou
 int ksched_run(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
     if (c->n_local < 0) return fail(c, KSCHED_E_STATE, "run before load_nodes");
-    if (c->o.nranks > 1 && !c->comm) return fail(c, KSCHED_E_STATE, "run: multi-rank context without ksched_set_comm");
+    if (c->o.nranks > 1 && !c->comm && !c->group)
+        return fail(c, KSCHED_E_STATE, "run: multi-rank context without ksched_set_comm / ksched_set_group");
     HIPCHK(c, hipSetDevice(c->dev));
     c->err.clear();
     c->st = ksched_stats{};
@@ -803,6 +993,7 @@ int ksched_run(ksched_ctx *c) {
     // the call's commits move every allocatable by at most the sum of the staged requests: keep the
     // FAST53 bound true of the state the NEXT call starts from
     if (r == KSCHED_OK) c->max_abs_alloc = sat_add(c->max_abs_alloc, c->sum_abs_req);
+    c->explain_valid = r == KSCHED_OK;
     return r;
 }
 

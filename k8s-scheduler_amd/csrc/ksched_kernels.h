@@ -195,6 +195,26 @@ constexpr size_t commit_lp_lds_bytes(int K) {
 static_assert(commit_lp_lds_bytes(16) <= 160 * 1024, "k_commit_lp LDS");
 constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
 
+// FailedScheduling diagnostics of a whole schedule call (ksched_explain.hip).
+struct ExplainArgs {
+    const int32_t *idx;           // the call's results (global node index | NO_FIT | NO_POSITIVE_SCORE)
+    int64_t p;
+    const int64_t *rc, *rm, *rp;  // the call's pods
+    const uint64_t *sel;
+    const NodeRec *nodes;         // this rank's node rows after the call
+    int64_t n_local, node_lo;
+    bool use_labels;
+    int32_t *fpod_out;            // explain_batch: the NO_FIT pods, in pod order (device, >= p entries)
+    int64_t *n_nofit;             // explain_batch: their number (host)
+    int64_t q_rc, q_rm, q_rp;     // explain_pod_at: that pod's request
+    uint64_t q_sel;
+};
+// counts[f][kNumReasons] (zeroed by the caller) for the f-th NO_FIT pod; ws is a growable workspace.
+hipError_t explain_batch(const ExplainArgs &a, void **ws, size_t *ws_bytes, unsigned long long *counts, hipStream_t s);
+// per-node reasons + counts of ONE pod against the state it saw at its turn (state: 3 * n_local int64)
+hipError_t explain_pod_at(const ExplainArgs &a, int64_t pod, int64_t *state, uint8_t *reason,
+                          unsigned long long *counts, hipStream_t s);
+
 // host-side launchers (ksched_kernels.hip).  fast53: every allocatable and request magnitude stays
 // below 2^52 for the whole call (host-checked), enabling (double)(a-r) == (double)a - (double)r.
 hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s);

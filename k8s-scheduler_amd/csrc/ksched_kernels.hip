@@ -270,26 +270,15 @@ __device__ __forceinline__ void score_topk_body(const ScoreArgs &A) {
 #pragma unroll
     for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
     int32_t cnt = 0;
-    for (int64_t j = sub; j < A.n_local; j += NSC) {
-        const NodeRec &nd = A.nodes[j];
-        int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
-        double af0 = nd.af[0], af1 = nd.af[1], af2 = nd.af[2], y0 = nd.y[0], y1 = nd.y[1], y2 = nd.y[2];
-        if (anyp) {  // wave-uniform: this sub-chunk holds committed nodes of batch b-2
-            const uint64_t hit = __ballot(pj0 == j || pj1 == j);
-            if (hit) {
-                const int src = __ffsll((unsigned long long)hit) - 1;
-                const int e = __builtin_amdgcn_readlane(pj0 == j ? lane : lane + 64, src);
-                const XRec &xr = A.patch->e[e];
-                ac = xr.cur[0]; am = xr.cur[1]; ap = xr.cur[2];
-                af0 = (double)ac; af1 = (double)am; af2 = (double)ap;
-                y0 = recip_or_zero(ac, af0); y1 = recip_or_zero(am, af1); y2 = recip_or_zero(ap, af2);
-            }
-        }
-        const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
+    // one node against this lane's pod: predicate, key, sorted insert (strict '>': nodes arrive in
+    // ascending index, so equal keys keep index order)
+    auto visit = [&](int64_t j, int64_t ac, int64_t am, int64_t ap, double af0, double af1, double af2, double y0,
+                     double y1, double y2, uint64_t lab, float price) {
+        const bool f = fits(rc, rm, rp, sel, ac, am, ap, lab, LAB);
         cnt += f;
         double k;
         const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, af0, af1, af2, y0, y1,
-                                                      y2, y3, nd.price, &k);
+                                                      y2, y3, price, &k);
         double ck = el ? k : -__builtin_inf();
         int32_t ci = (int32_t)(A.node_offset + j);
         bool moved = false;  // once placed, every later entry shifts down one slot
@@ -301,6 +290,40 @@ __device__ __forceinline__ void score_topk_body(const ScoreArgs &A) {
             const int32_t ti = idx[q];
             key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
             ck = sw ? tk : ck; ci = sw ? ti : ci;
+        }
+    };
+    if (!anyp) {
+        // Node rows are wave-uniform: read through the constant address space they arrive as scalar
+        // loads (s_load_dwordx16 + x8) into SGPRs, one row ahead of its use -- row j + NSC is in flight
+        // while row j is scored -- and feed the VALU as scalar operands (no row VGPRs).
+        const NodeRecC *rows = (const NodeRecC *)(A.nodes);
+        NodeRec nxt;
+        if (sub < A.n_local) nxt = load_row(rows + sub);
+        for (int64_t j = sub; j < A.n_local; j += NSC) {
+            const NodeRec nd = nxt;
+            const int64_t jn = j + NSC;
+            if (jn < A.n_local) nxt = load_row(rows + jn);
+            visit(j, nd.a[0], nd.a[1], nd.a[2], nd.af[0], nd.af[1], nd.af[2], nd.y[0], nd.y[1], nd.y[2], nd.labels,
+                  nd.price);
+        }
+    } else {
+        // this sub-chunk holds nodes committed by batch b-2 (~6 % of the waves at B = 64): their rows
+        // are overlaid from the XBuf as they are reached (the write-back above may not be visible yet
+        // to this launch's reads, and is not done at all by pod groups y > 0)
+        for (int64_t j = sub; j < A.n_local; j += NSC) {
+            const NodeRec &nd = A.nodes[j];
+            int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+            double af0 = nd.af[0], af1 = nd.af[1], af2 = nd.af[2], y0 = nd.y[0], y1 = nd.y[1], y2 = nd.y[2];
+            const uint64_t hit = __ballot(pj0 == j || pj1 == j);
+            if (hit) {
+                const int src = __ffsll((unsigned long long)hit) - 1;
+                const int e = __builtin_amdgcn_readlane(pj0 == j ? lane : lane + 64, src);
+                const XRec &xr = A.patch->e[e];
+                ac = xr.cur[0]; am = xr.cur[1]; ap = xr.cur[2];
+                af0 = (double)ac; af1 = (double)am; af2 = (double)ap;
+                y0 = recip_or_zero(ac, af0); y1 = recip_or_zero(am, af1); y2 = recip_or_zero(ap, af2);
+            }
+            visit(j, ac, am, ap, af0, af1, af2, y0, y1, y2, nd.labels, nd.price);
         }
     }
     if (cnt) atomicAdd(&s_cnt[lane], cnt);
@@ -554,7 +577,9 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
 // workgroups, all already dispatched or dispatchable: no early-resident consumers) and merge one pod
 // each, so no merge kernel and no score -> merge queue hand-off exist.
 template <int KC, int PRIO, int DOM, bool LAB, bool F53, bool FUSE>
-__global__ __launch_bounds__(kScoreThreads) void k_score_topk(ScoreArgs A, MergeArgs M) {
+// <= 64 VGPRs (launch bound: 8 waves per SIMD): two score waves + two commit waves (190 VGPRs) must
+// fit one SIMD, or the single-workgroup commit cannot dispatch beside the score grid.
+__global__ __launch_bounds__(kScoreThreads, 8) void k_score_topk(ScoreArgs A, MergeArgs M) {
     score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
     if constexpr (FUSE) {
         static_assert(kScoreThreads == kMergeThreads, "fused merge runs one pod per score workgroup");

@@ -8,8 +8,8 @@ Product surface:
 """
 from ._lib import (DOMAIN_ALL, DOMAIN_FEASIBLE, MODE_AUTO, MODE_BATCHED, MODE_EXACT, NO_FIT, NO_POSITIVE_SCORE,
                    PRIORITY_BEST_PRICE, PRIORITY_RESOURCE, KschedError, lib)
-from .engine import Engine, engine_for
+from .engine import Engine, Group, engine_for
 
-__all__ = ["Engine", "engine_for", "KschedError", "lib", "MODE_AUTO", "MODE_BATCHED", "MODE_EXACT",
+__all__ = ["Engine", "Group", "engine_for", "KschedError", "lib", "MODE_AUTO", "MODE_BATCHED", "MODE_EXACT",
            "PRIORITY_RESOURCE", "PRIORITY_BEST_PRICE", "DOMAIN_ALL", "DOMAIN_FEASIBLE", "NO_FIT",
            "NO_POSITIVE_SCORE"]

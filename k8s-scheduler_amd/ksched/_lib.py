@@ -76,9 +76,14 @@ SIGNATURES = [
     ("ksched_last_error", C.c_char_p, [CTX]),
     ("ksched_get_unique_id", C.c_int, [C.c_char_p]),
     ("ksched_set_comm", C.c_int, [CTX, C.c_char_p]),
+    ("ksched_group_create", C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("ksched_group_destroy", C.c_int, [C.c_void_p]),
+    ("ksched_set_group", C.c_int, [CTX, C.c_void_p]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
     ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),
+    ("ksched_explain_batch", C.c_int, [CTX, C.c_int64, I64P, I64P]),
+    ("ksched_explain_pod", C.c_int, [CTX, C.c_int64, I64P, C.POINTER(C.c_uint8)]),
     ("ksched_read_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P]),
     ("ksched_save_state", C.c_int, [CTX]),
     ("ksched_restore_state", C.c_int, [CTX]),

@@ -24,7 +24,7 @@ DECIMAL_CPU = ("0.1", "0.15", "0.2", "0.25", "0.3", "0.35", "0.4", "0.5", "0.6",
 
 HC_USED_LO, HC_USED_SPAN = 0.97, 0.027  # c5hc node usage (cpu and memory)
 HC_POD_SCALE = 1                        # c5hc pod requests relative to the standard pods
-HC_HOT_EVERY = 100                      # c5hc: one fresh large node per this many nodes
+HC_HOT_EVERY = 50                       # c5hc: one fresh large node per this many nodes
 
 PRIORITY_RESOURCE = 0
 PRIORITY_BEST_PRICE = 1
@@ -100,7 +100,7 @@ CONFIGS = {
     "c4": (100_000, 1_000_000, PRIORITY_RESOURCE, DOMAIN_ALL, False, "batched"),
     "c5": (200_000, 500_000, PRIORITY_RESOURCE, DOMAIN_FEASIBLE, True, "batched"),
     # c5 made genuinely high-conflict: nodes 97-99.7 % used except one fresh large
-    # node in every 100, so every batch piles onto the same few fresh nodes -- placements re-touch
+    # node in every 50, so every batch piles onto the same few fresh nodes -- placements re-touch
     # nodes of the batch, and most batches exhaust some pod's candidate list (truncation + re-score)
     "c5hc": (200_000, 500_000, PRIORITY_RESOURCE, DOMAIN_FEASIBLE, True, "batched"),
 }

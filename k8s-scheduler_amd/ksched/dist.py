@@ -37,8 +37,10 @@ def broadcast_bytes(payload, rank: int, src: int = 0) -> bytes:
     return obj[0]
 
 
-def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, **kw):
-    """Engine for this rank's node shard of cluster `cl`; RCCL communicator set up when world > 1."""
+def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group=None, **kw):
+    """Engine for this rank's node shard of cluster `cl`.  world > 1: joined to the other ranks by an
+    RCCL communicator (one process per GPU, torch.distributed hands out the id), or -- `group` given --
+    by an in-process rank group (ranks as threads of this process on one device)."""
     from . import _lib as L
     from .engine import Engine
     lo, hi = shard_range(cl.n_nodes, rank, world)
@@ -49,7 +51,9 @@ def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, **kw)
     eng.load_nodes(cl.alloc_cpu[lo:hi], cl.alloc_mem[lo:hi], cl.alloc_pods[lo:hi],
                    labels=None if cl.labels is None else cl.labels[lo:hi],
                    price=None if cl.price is None else cl.price[lo:hi])
-    if world > 1:
+    if group is not None:
+        eng.set_group(group)
+    elif world > 1:
         uid = Engine.unique_id() if rank == 0 else None
         uid = broadcast_bytes(uid, rank)
         eng.set_comm(uid)

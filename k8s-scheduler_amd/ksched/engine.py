@@ -22,6 +22,29 @@ def _i64(a):
     return np.ascontiguousarray(a, dtype=np.int64)
 
 
+class Group:
+    """In-process rank group (ksched_group): R contexts of this process on one device exchange their
+    per-batch candidate lists through a shared device ring instead of RCCL.  Each rank's Engine calls
+    set_group(); the ranks then run the same schedule calls concurrently (one thread each)."""
+
+    def __init__(self, nranks: int, device: int = -1):
+        h = C.c_void_p()
+        L.check(L.lib().ksched_group_create(int(nranks), int(device), C.byref(h)), what="group_create")
+        self._h = h
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib().ksched_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Engine:
     def __init__(self, mode: int = L.MODE_AUTO, priority: int = L.PRIORITY_RESOURCE, domain: int = L.DOMAIN_ALL,
                  use_labels: bool = False, batch: int = 0, topk: int = 0, device: int = -1,
@@ -74,6 +97,10 @@ class Engine:
         assert len(uid) == 128
         self._chk(L.lib().ksched_set_comm(self._ctx, uid), "set_comm")
 
+    def set_group(self, group: "Group"):
+        self._chk(L.lib().ksched_set_group(self._ctx, group._h), "set_group")
+        self._group = group  # keep the group alive as long as this context
+
     # -- nodes ---------------------------------------------------------------------------------
     def load_nodes(self, alloc_cpu, alloc_mem, alloc_pods, labels=None, price=None):
         ac, am, ap = _i64(alloc_cpu), _i64(alloc_mem), _i64(alloc_pods)
@@ -99,6 +126,24 @@ class Engine:
         rs = np.empty(max(self.n, 0), np.uint8) if per_node else None
         self._chk(L.lib().ksched_explain(self._ctx, int(req_cpu), int(req_mem), int(req_pods), int(selector),
                                          L.ptr(cnt, C.c_int64), L.ptr(rs, C.c_uint8)), "explain")
+        return cnt, rs
+
+    def explain_batch(self):
+        """Reason counts (int64[p, NUM_REASONS]) of every NO_FIT pod of the last schedule call at its
+        own turn, computed on the device; rows of other pods are zero.  Returns (counts, n_nofit)."""
+        cnt = np.zeros((self.p, L.NUM_REASONS), np.int64)
+        nf = C.c_int64(0)
+        self._chk(L.lib().ksched_explain_batch(self._ctx, self.p, L.ptr(cnt, C.c_int64), C.byref(nf)),
+                  "explain_batch")
+        return cnt, nf.value
+
+    def explain_pod(self, pod: int, per_node: bool = True):
+        """Per-node reasons of pod `pod` of the last schedule call against the state it saw at its turn.
+        Returns (counts int64[NUM_REASONS], reasons uint8[n] | None)."""
+        cnt = np.zeros(L.NUM_REASONS, np.int64)
+        rs = np.empty(max(self.n, 0), np.uint8) if per_node else None
+        self._chk(L.lib().ksched_explain_pod(self._ctx, int(pod), L.ptr(cnt, C.c_int64), L.ptr(rs, C.c_uint8)),
+                  "explain_pod")
         return cnt, rs
 
     def read_nodes(self):

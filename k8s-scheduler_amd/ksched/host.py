@@ -290,29 +290,11 @@ class FakeCluster:
                  for j, r in enumerate(reasons) if r != L.REASON_FIT]
         return f"pod ({pod.name}) failed to fit in any node\n" + "\n".join(lines)
 
-    def _explain_failures(self, pending, rc, rm, rp, sel, idx):
-        """Per-node reasons of every NO_FIT pod at ITS turn.  The engine's state after the call is
-        the state after the last pod; walking backwards, each placed pod after a failed pod is
-        credited back (apply_delta), so the state seen by explain() equals the one the failed pod
-        saw; the credits are then charged again.  All arithmetic is the device's wrapping int64."""
-        fails = [i for i, x in enumerate(idx) if x == L.NO_FIT]
-        if not fails:
-            return {}
-        out = {}
-        credited = []
-        hi = len(pending)
-        for i in reversed(fails):
-            back = [j for j in range(i + 1, hi) if idx[j] >= 0]
-            if back:
-                self.engine.apply_delta([int(idx[j]) for j in back], [int(rc[j]) for j in back],
-                                        [int(rm[j]) for j in back], [1] * len(back))
-                credited += back
-            out[i] = self.engine.explain(rc[i], rm[i], rp[i], 0 if sel is None else int(sel[i]))[1]
-            hi = i
-        if credited:
-            self.engine.apply_delta([int(idx[j]) for j in credited], [-int(rc[j]) for j in credited],
-                                    [-int(rm[j]) for j in credited], [-1] * len(credited))
-        return out
+    def _explain_failures(self, idx):
+        """Per-node reasons of every NO_FIT pod of the call just made, each against the state it saw at
+        its own turn -- reconstructed on the device from the call's placements (ksched_explain_pod),
+        no host replay and no state change."""
+        return {i: self.engine.explain_pod(i)[1] for i, x in enumerate(idx) if x == L.NO_FIT}
 
     def bind(self, pod: Pod, node: Node) -> None:
         """POST Binding + Scheduled event (anchor/schedule.go:200-261), in memory."""
@@ -330,7 +312,7 @@ class FakeCluster:
             selectors = [self.selector_of(p) for p in pending]
         sel = None if not self.use_labels else np.asarray(selectors, dtype=np.uint64)
         idx, score, feas = self.engine.schedule(rc, rm, rp, sel)
-        why = self._explain_failures(pending, rc, rm, rp, sel, idx) if self.explain_failures else {}
+        why = self._explain_failures(idx) if self.explain_failures else {}
         out = []
         for k, (pod, i) in enumerate(zip(pending, idx)):
             if i == L.NO_FIT:
