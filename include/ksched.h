@@ -50,7 +50,7 @@ extern "C" {
 
 /* ordered-commit implementations (batched mode; all produce the sequential result) */
 #define KSCHED_COMMIT_SEQUENTIAL 1    /* one wave re-scores the touched set per pod (batch <= 128) */
-#define KSCHED_COMMIT_LANE_PER_POD 2  /* one wave, lane = pod, incremental pod x touched-node keys (batch <= 64) */
+#define KSCHED_COMMIT_LANE_PER_POD 2  /* retired (round 1 variant): treated as KSCHED_COMMIT_SPECULATIVE */
 #define KSCHED_COMMIT_SPECULATIVE 3   /* guess first touches, check all pods in parallel, resolve the first miss (batch <= 64) */
 
 #define KSCHED_DOMAIN_ALL 0       /* argmax over ALL nodes, feasible or not (the reference, anchor/priorities.go:45) */

@@ -1,6 +1,6 @@
 // ksched_commit_spc.hip -- ordered commit of one speculative batch by speculation + parallel check.
 //
-// Same result as the sequential replay (k_commit / k_commit_lp): pods of the batch
+// Same result as the sequential replay (k_commit): pods of the batch
 // in order, each seeing every placement before it (anchor/schedule.go:185-197).  Instead of deciding
 // one pod at a time, a round
 //   1. (wave 0, integer work only) GUESSES every remaining pod's placement: its first list entry that
@@ -16,7 +16,7 @@
 // Placements are first touches almost always (99.4 % on BASELINE c4), so a batch usually takes one or
 // two rounds.  The guess window adapts (halves around failures) to bound the cost of adversarial
 // batches.  The lists, cut rule, touched-set inheritance, export, plan and truncation are those of
-// k_commit_lp.
+// k_commit.
 #include <hip/hip_runtime.h>
 
 #include "ksched_kernels.h"
@@ -108,8 +108,10 @@ __device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64
 
 }  // namespace
 
+// <= 192 VGPRs (amdgpu_num_vgpr counts half the unified gfx950 file): beside a resident score workgroup (two 64-VGPR waves per SIMD) the commit's two waves
+// per SIMD must fit the 512-entry file, or a score grid polling for this commit would never let it in.
 template <int K, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
+__global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) void k_commit_spc(CommitArgs A) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x;
@@ -119,10 +121,13 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
     const int64_t cursor = A.ctl->cursor;
     if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
         // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
-        if (tid == 0) {
-            A.xout->count = 0;
-            if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
-            plan_after_commit(A, false, cursor);
+        if (wave == 0) {
+            if (lane == 0) {
+                A.xout->count = 0;
+                if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
+                plan_after_commit(A, false, cursor);
+            }
+            publish_committed(A);
         }
         return;
     }
@@ -562,6 +567,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_commit_spc(CommitArgs A) {
             A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
         }
     }
+    publish_committed(A);  // wave 0 made every global store of this kernel
 }
 
 namespace {
@@ -599,6 +605,27 @@ hipError_t commit_spc_k(int K, const CommitArgs &a, hipStream_t s) {
 }
 
 }  // namespace
+
+namespace {
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t spc_attr_one(hipFuncAttributes *at, size_t *lds) {
+    *lds = spc_lds_bytes<K>();
+    return hipFuncGetAttributes(at, (const void *)k_commit_spc<K, PRIO, DOM, LAB, F53>);
+}
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t spc_attr_k(int K, hipFuncAttributes *at, size_t *lds) {
+    switch (K) {
+        case 4: return spc_attr_one<4, PRIO, DOM, LAB, F53>(at, lds);
+        case 8: return spc_attr_one<8, PRIO, DOM, LAB, F53>(at, lds);
+        case 16: return spc_attr_one<16, PRIO, DOM, LAB, F53>(at, lds);
+        default: return hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+hipError_t commit_spc_attributes(int K, int prio, int dom, bool lab, bool f53, hipFuncAttributes *at, size_t *lds) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (spc_attr_k<P_, D_, L_, F_>(K, at, lds)));
+}
 
 hipError_t launch_commit_spc(int K, int prio, int dom, bool lab, bool f53, const CommitArgs &a, hipStream_t s) {
     if (a.B > 64) return hipErrorInvalidValue;

@@ -88,8 +88,7 @@ struct ksched_ctx {
     int64_t *h_cursor = nullptr;  // pinned
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
     int64_t *d_mdbg = nullptr;    // KSCHED_MERGE_STAMPS diagnostics
-    hipStream_t stream2 = nullptr;  // commit stream of the batched pipeline
-    hipStream_t stream3 = nullptr;  // merge (+ rank exchange) stream of the batched pipeline
+    hipStream_t stream2 = nullptr;  // merge + commit stream of the batched pipeline
     hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[2] = {};
     void *d_xring = nullptr, *d_lring = nullptr;
     int64_t xring_bytes = 0, lring_bytes = 0;
@@ -257,13 +256,17 @@ int decide_fast53(ksched_ctx *c) {
 }
 
 // Batched mode, software-pipelined over two streams:
-//   stream S: [wait commit(b-2)] score(b) (+ overlay/write-back of b-2's commits) -> merge(b)
-//             [-> all-gather -> rank merge]
-//   stream C: [wait lists(b)]    commit(b) (+ plan of batch b+2)
+//   stream S: score(b)                     polls Ctl::committed >= b - 1 (commit(b-2) done) on the device,
+//                                          then overlays / writes back b-2's commits as it scans
+//   stream C: merge(b) [-> all-gather -> rank merge] -> commit(b)  (+ plan of batch b+2, publish)
 // score(b) runs on every CU while commit(b-1) runs on one; commit(b) inherits the nodes committed by
 // batch b-1 (its score snapshot is one batch older).  Each batch's start is planned speculatively
 // (previous start + B) by the commit two batches back; a truncated batch invalidates the in-flight
 // speculation, which commit skips, and plans its restart at the committed frontier.
+// The commit(b-2) -> score(b) edge is a device-side flag (score(b) is already resident when it is
+// released: ~2 us) instead of a cross-queue stream event (~13 us per batch measured on MI355X, even
+// when the event has completed: profiles/r02_*).  score(b) -> merge(b) stays an event unless the merge
+// polls Ctl::scored (KSCHED_DEVICE_HANDOFF=1).
 int enqueue_batched(ksched_ctx *c) {
     const BatchPlan pl = plan_batch(c);
     if (c->ws_bytes < (int64_t)pl.total) {
@@ -281,32 +284,17 @@ int enqueue_batched(ksched_ctx *c) {
     const bool lab = c->o.use_labels != 0;
     const int R = std::max(1, c->o.nranks);
     PodArgs pods{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
-    const int poll = env_int("KSCHED_POLL_BATCHES", 0);
     const bool f53 = c->fast53;
-    const bool one_stream = env_int("KSCHED_ONE_STREAM", 0) != 0;
-    // commit implementation: speculative-parallel (B <= 64, default), lane-per-pod (B <= 64), or the
-    // single-wave sequencer (any B <= 128)
-    int impl = c->o.commit_impl ? c->o.commit_impl : env_int("KSCHED_COMMIT_IMPL", 0);
-    if (impl == 0) impl = pl.B <= 64 ? KSCHED_COMMIT_SPECULATIVE : KSCHED_COMMIT_SEQUENTIAL;
+    // commit implementation: speculative-parallel (B <= 64, default) or the single-wave sequencer (B <= 128)
+    int impl = c->o.commit_impl ? c->o.commit_impl : KSCHED_COMMIT_SPECULATIVE;
     if (impl != KSCHED_COMMIT_SEQUENTIAL && pl.B > 64) impl = KSCHED_COMMIT_SEQUENTIAL;
-    const bool lp_commit = impl == KSCHED_COMMIT_LANE_PER_POD;
-    const bool spc_commit = impl == KSCHED_COMMIT_SPECULATIVE;
-    // merge and commit share stream C by default: the hand-off merge(b) -> commit(b) is then an
-    // in-queue dependency (~2 us) instead of a cross-queue event wait (~12 us, tools/trace_gaps.py);
-    // KSCHED_MC_SPLIT=1 restores a separate merge stream.
-    const bool mc_split = env_int("KSCHED_MC_SPLIT", 0) != 0;
-    hipStream_t sS = c->stream, sC = one_stream ? c->stream : c->stream2;
-    hipStream_t sM = one_stream ? c->stream : (mc_split ? c->stream3 : c->stream2);
-    // score(b) -> merge(b) is a cross-queue event wait (~12 us).  KSCHED_DEVICE_HANDOFF=1 makes the
-    // merge poll Ctl::scored on the device instead: measured c4 +4%, but c5 -19% (the 64 early-resident
-    // merge workgroups take slots the score grid needs: score 82 -> 110 us), so it is off by default.
-    const bool dev_handoff = !one_stream && env_int("KSCHED_DEVICE_HANDOFF", 0) != 0;
+    const bool spc_commit = impl != KSCHED_COMMIT_SEQUENTIAL;
+    hipStream_t sS = c->stream, sC = c->stream2;
+    // device-side score wait only where the commit provably fits beside a resident score workgroup
+    const bool score_poll = env_int("KSCHED_SCORE_EVENT", 0) == 0 &&
+                            commit_fits_beside_score(pl.KC, pl.K, pl.B, spc_commit, prio, dom, lab, f53);
+    const bool dev_handoff = env_int("KSCHED_DEVICE_HANDOFF", 0) != 0;
     unsigned long long scored_target = 0;
-    // Fused merge (KSCHED_FUSE_MERGE=1; single rank, KC 4 / K 16, one pod group, >= B score workgroups):
-    // parity-green but measured slower (c4 7.5e10 vs 1.05e11: score+merge 75 us vs 47+15, and the
-    // commit co-running with it 71 us vs 37), so the separate merge kernel stays the default.
-    const bool fuse = !one_stream && !dev_handoff && !c->comm && !c->group && pl.KC == 4 && pl.K == 16 && pl.pod_groups == 1 &&
-                      pl.n_chunks / kScoreWaves >= pl.B && !c->d_mdbg && env_int("KSCHED_FUSE_MERGE", 0) != 0;
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -332,16 +320,13 @@ int enqueue_batched(ksched_ctx *c) {
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
     if (env_int("KSCHED_MERGE_STAMPS", 0) && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
     if (c->d_mdbg) HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), sS));
-    if (!one_stream) {  // streams M and C start after the initialisation above
-        HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));
-        HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
-        if (sM != sC) HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
-    }
-    int64_t resolved = 0, b = 0, last_resolved_b = -1;
+    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // stream C starts after the initialisation above
+    HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
+    int64_t resolved = 0, b = 0;
     double avg_progress = std::max(1.0, pl.B * 0.75);
     while (resolved < c->p) {
         int64_t m = (int64_t)std::ceil((double)(c->p - resolved) / avg_progress) + 2;
-        m = std::max<int64_t>(2, std::min<int64_t>(m, poll > 0 ? poll : 256));
+        m = std::max<int64_t>(2, std::min<int64_t>(m, 256));
         const int64_t b_end = b + m;
         for (; b < b_end; ++b) {
             const bool tm = c->o.timing && (b % (c->o.timing_every > 0 ? c->o.timing_every : 16) == 0);
@@ -351,20 +336,20 @@ int enqueue_batched(ksched_ctx *c) {
             char *lists_base = static_cast<char *>(c->d_lring) + (size_t)(b % kRing) * pl.send_bytes;
             // S: score b once commit(b-2) is done (its plan for b and its committed nodes, which score(b)
             // overlays on the rows it reads and writes back)
-            if (b >= 2 && !one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[(b - 2) % kRing], 0));
             ScoreArgs sa{};
+            if (b >= 2) {
+                if (score_poll) { sa.wait_committed = &ctl->committed; sa.wait_target = (unsigned long long)(b - 1); }
+                else HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[(b - 2) % kRing], 0));
+            }
+            sa.err = c->d_err;
             sa.nodes = c->d_nodes; sa.n_local = c->n_local; sa.node_offset = c->o.node_offset;
             sa.S = pl.S; sa.n_chunks = pl.n_chunks; sa.pods = pods; sa.cursor = plan; sa.B = pl.B;
             const size_t part_elems = (size_t)pl.B * pl.C[0];
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part) + (size_t)(b % 2) * part_elems * pl.KC;
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt) + (size_t)(b % 2) * part_elems;
             sa.patch = xbuf(b - 2);
-            const unsigned long long g_launch = (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
-            sa.done = (dev_handoff || fuse) ? &ctl->scored : nullptr;
-            sa.fuse_merge = fuse ? 1 : 0;
-            sa.g_total = (int32_t)g_launch;
-            sa.done_base = scored_target;
-            scored_target += g_launch;
+            sa.done = dev_handoff ? &ctl->scored : nullptr;
+            scored_target += (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
             MergeArgs ma{};
             ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
             ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
@@ -376,53 +361,44 @@ int enqueue_batched(ksched_ctx *c) {
             ma.out_rec = reinterpret_cast<Rec *>(lists_base);
             ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
             HIPCHK(c, ev_begin(c, tm, &e0, sS));
-            HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, ma, pl.pod_groups, sS));
+            HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
-            // M: merge b while stream S scores b+1 (the lists' part buffers alternate)
-            if (fuse) {  // score(b) produced the merged lists: commit(b) waits for it directly
+            // C: merge b while stream S scores b+1 (the lists' part buffers alternate)
+            if (!dev_handoff) {
                 HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
                 HIPCHK(c, hipStreamWaitEvent(sC, c->ev_scored[b % kRing], 0));
-            } else {
-                if (!one_stream && !dev_handoff) {
-                    HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
-                    HIPCHK(c, hipStreamWaitEvent(sM, c->ev_scored[b % kRing], 0));
-                }
-                HIPCHK(c, ev_begin(c, tm, &e0, sM));
-                HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sM));
-                HIPCHK(c, ev_end(c, tm, 1, e0, 0, sM));
             }
+            HIPCHK(c, ev_begin(c, tm, &e0, sC));
+            HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sC));
+            HIPCHK(c, ev_end(c, tm, 1, e0, 0, sC));
             const Rec *lists = reinterpret_cast<const Rec *>(lists_base);
             const int64_t *fc0 = reinterpret_cast<const int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
             if (c->comm || c->group) {  // node-sharded: exchange the local lists (a 1-rank communicator also takes this path)
-                HIPCHK(c, ev_begin(c, tm, &e0, sM));
+                HIPCHK(c, ev_begin(c, tm, &e0, sC));
                 if (c->comm) {
-                    NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sM));
+                    NCCLCHK(c, ncclAllGather(lists_base, ws + pl.off_recv, pl.send_bytes, ncclUint8, c->comm, sC));
                 } else {
                     ksched_group *g = c->group;
                     int dummy;
-                    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sM));
+                    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sC));
                     HIPCHK(c, hipEventSynchronize(c->ev_pipe[0]));  // my block is final
                     g->send[(size_t)c->o.rank] = lists_base;
                     if (!group_min(g, 0, &dummy)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer stopped exchanging");
                     for (int q = 0; q < R; ++q)
                         HIPCHK(c, hipMemcpyAsync(ws + pl.off_recv + (size_t)q * pl.send_bytes, g->send[(size_t)q],
-                                                 pl.send_bytes, hipMemcpyDeviceToDevice, sM));
-                    HIPCHK(c, hipStreamSynchronize(sM));
+                                                 pl.send_bytes, hipMemcpyDeviceToDevice, sC));
+                    HIPCHK(c, hipStreamSynchronize(sC));
                     if (!group_min(g, 0, &dummy)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer stopped exchanging");
                 }
-                MergeArgs ma{};
-                ma.in = ws + pl.off_recv; ma.rank_stride = (int64_t)pl.send_bytes; ma.C_in = R; ma.C_out = 1;
-                ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
-                ma.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists) + (size_t)(b % 2) * pl.B * pl.K;
-                ma.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc) + (size_t)(b % 2) * pl.B;
-                HIPCHK(c, launch_merge(pl.K, pl.K, true, true, ma, sM));
-                lists = ma.out_rec;
-                fc0 = ma.out_fc;
-                HIPCHK(c, ev_end(c, tm, 3, e0, 0, sM));
-            }
-            if (sM != sC && !fuse) {
-                HIPCHK(c, hipEventRecord(c->ev_lists[b % kRing], sM));
-                HIPCHK(c, hipStreamWaitEvent(sC, c->ev_lists[b % kRing], 0));
+                MergeArgs mr{};
+                mr.in = ws + pl.off_recv; mr.rank_stride = (int64_t)pl.send_bytes; mr.C_in = R; mr.C_out = 1;
+                mr.cursor = plan; mr.P = c->p; mr.B = pl.B;
+                mr.out_rec = reinterpret_cast<Rec *>(ws + pl.off_glists) + (size_t)(b % 2) * pl.B * pl.K;
+                mr.out_fc = reinterpret_cast<int64_t *>(ws + pl.off_gfc) + (size_t)(b % 2) * pl.B;
+                HIPCHK(c, launch_merge(pl.K, pl.K, true, true, mr, sC));
+                lists = mr.out_rec;
+                fc0 = mr.out_fc;
+                HIPCHK(c, ev_end(c, tm, 3, e0, 0, sC));
             }
             // C: ordered commit of batch b
             CommitArgs ca{};
@@ -432,12 +408,12 @@ int enqueue_batched(ksched_ctx *c) {
             ca.xin = xbuf(b - 1); ca.xout = xbuf(b);
             ca.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
             ca.dbg = c->d_dbg;
+            ca.batch = b;
             HIPCHK(c, ev_begin(c, tm, &e0, sC));
             if (spc_commit) HIPCHK(c, launch_commit_spc(pl.K, prio, dom, lab, f53, ca, sC));
-            else if (lp_commit) HIPCHK(c, launch_commit_lp(pl.K, prio, dom, lab, f53, ca, sC));
             else HIPCHK(c, launch_commit(pl.K, prio, dom, lab, f53, ca, (size_t)lds, sC));
             HIPCHK(c, ev_end(c, tm, 2, e0, 0, sC));
-            if (!one_stream) HIPCHK(c, hipEventRecord(c->ev_commit[b % kRing], sC));
+            HIPCHK(c, hipEventRecord(c->ev_commit[b % kRing], sC));
         }
         HIPCHK(c, hipMemcpyAsync(c->h_cursor, ctl, sizeof(Ctl), hipMemcpyDeviceToHost, sC));
         HIPCHK(c, hipStreamSynchronize(sC));
@@ -445,18 +421,15 @@ int enqueue_batched(ksched_ctx *c) {
         if (h->cursor <= resolved) return fail(c, KSCHED_E_DEVICE, "batched mode made no progress");
         resolved = h->cursor;
         if (h->stats[0] > 0) avg_progress = std::max(1.0, (double)resolved / (double)(b));
-        last_resolved_b = b;
     }
-    (void)last_resolved_b;
     // drain: write back the last two batches' commits (the others were applied in the pipeline)
     for (int64_t bb = std::max<int64_t>(0, b - 2); bb < b; ++bb) {
-        if (!one_stream) HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[bb % kRing], 0));
+        HIPCHK(c, hipStreamWaitEvent(sS, c->ev_commit[bb % kRing], 0));
         HIPCHK(c, launch_apply_batch(xbuf(bb), c->d_nodes, c->o.node_offset, c->n_local, sS));
     }
-    if (!one_stream) {  // the run's end event is recorded on stream S: make it cover stream C
-        HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));
-        HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
-    }
+    // the run's end event is recorded on stream S: make it cover stream C
+    HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));
+    HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
     if (c->d_mdbg) {
         int64_t hm[8];
         HIPCHK(c, hipStreamSynchronize(sS));
@@ -482,18 +455,11 @@ int enqueue_batched(ksched_ctx *c) {
                          (long long)hd[14], (long long)hd[12], (long long)hd[13], (double)hd[12] / (hd[14] ? hd[14] : 1),
                          (double)hd[0] / hd[14], (double)hd[1] / hd[14], (double)hd[2] / hd[14], (double)hd[3] / hd[14],
                          (double)hd[4] / hd[14]);
-        else if (lp_commit)
-            std::fprintf(stderr, "[ksched commit_lp stamps] pods=%lld kernels=%lld slots=%lld | cycles/kernel: prologue %.0f "
-                         "total %.0f | cycles/pod: reduce %.0f decide %.0f commit+score %.0f advance+out %.0f | skipped %lld | "
-                         "row re-reductions %lld, first touches %lld of %lld placed\n",
-                         (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[7], (double)hd[8] / hd[7],
-                         (double)hd[1] / hd[5], (double)hd[2] / hd[5], (double)hd[3] / hd[5], (double)hd[4] / hd[5],
-                         (long long)h->stats[3], (long long)hd[9], (long long)hd[10], (long long)hd[11]);
         else
-        std::fprintf(stderr, "[ksched commit stamps] pods=%lld kernels=%lld touched=%lld | cycles/pod: loads+rescore %.0f "
-                     "reduce %.0f decide %.0f commit+store %.0f | loop cycles/pod %.0f | skipped %lld\n",
-                     (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[5], (double)hd[1] / hd[5],
-                     (double)hd[2] / hd[5], (double)hd[3] / hd[5], (double)hd[4] / hd[5], (long long)h->stats[3]);
+            std::fprintf(stderr, "[ksched commit stamps] pods=%lld kernels=%lld touched=%lld | cycles/pod: loads+rescore %.0f "
+                         "reduce %.0f decide %.0f commit+store %.0f | loop cycles/pod %.0f | skipped %lld\n",
+                         (long long)hd[5], (long long)hd[7], (long long)hd[6], (double)hd[0] / hd[5], (double)hd[1] / hd[5],
+                         (double)hd[2] / hd[5], (double)hd[3] / hd[5], (double)hd[4] / hd[5], (long long)h->stats[3]);
     }
     return KSCHED_OK;
 }
@@ -573,7 +539,8 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->KC = std::min(c->K, opts->chunk_topk ? opts->chunk_topk : env_int("KSCHED_CHUNK_TOPK", 4));
     c->B = opts->batch > 0 ? opts->batch : std::min(128, 8 * c->K);
     if (c->B > 128) { delete c; return KSCHED_E_INVALID; }
-    if (opts->commit_impl < 0 || opts->commit_impl > 3) { delete c; return KSCHED_E_INVALID; }  // touched table: 2B <= 256 = 4 slots per lane
+    if (opts->commit_impl < 0 || opts->commit_impl > 3) { delete c; return KSCHED_E_INVALID; }
+    // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { delete c; return KSCHED_E_DEVICE; }
     if (opts->device >= 0) {
@@ -592,7 +559,6 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     for (int i = 0; i < 2; ++i) ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming) == hipSuccess;
     if (!ev_ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc((void **)&c->d_cursor, sizeof(Ctl)) != hipSuccess ||
         hipMalloc((void **)&c->d_err, sizeof(int32_t)) != hipSuccess ||
@@ -613,7 +579,6 @@ int ksched_destroy(ksched_ctx *c) {
     hipSetDevice(c->dev);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->stream2) hipStreamSynchronize(c->stream2);
-    if (c->stream3) hipStreamSynchronize(c->stream3);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
@@ -633,7 +598,6 @@ int ksched_destroy(ksched_ctx *c) {
     hipFree(c->d_xws); hipFree(c->d_xbuf);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
-    if (c->stream3) hipStreamDestroy(c->stream3);
     delete c;
     return KSCHED_OK;
 }
@@ -1017,9 +981,10 @@ int ksched_sync(ksched_ctx *c) {
     }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
-    if (e == 2) {
+    if (e == 2 || e == 4) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
-        return fail(c, KSCHED_E_DEVICE, "batched mode: the merge's wait for the score workgroups timed out");
+        return fail(c, KSCHED_E_DEVICE, e == 2 ? "batched mode: the merge's wait for the score workgroups timed out"
+                                               : "batched mode: the score's wait for commit(b-2) timed out");
     }
     if (e) return fail(c, KSCHED_E_DEVICE, "exact mode: cross-workgroup exchange timed out (workgroups not co-resident?)");
     return KSCHED_OK;

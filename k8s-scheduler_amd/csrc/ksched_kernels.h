@@ -59,7 +59,8 @@ struct alignas(8) Ctl {
     int64_t resync;     // 1: a batch truncated; the next plan restarts at cursor
     int64_t stats[5];   // batches committed, truncated, placed, skipped, pairs scored
     int64_t plan[kPlanRing];
-    unsigned long long scored;  // score workgroups finished this call (device hand-off to the merge)
+    unsigned long long scored;     // score workgroups finished this call (device hand-off to the merge)
+    unsigned long long committed;  // batches committed this call: commit(b) publishes b + 1 (release)
 };
 
 struct PodArgs {
@@ -99,10 +100,10 @@ struct ScoreArgs {
     int64_t *part_cnt; // [B][workgroups]
     const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
     unsigned long long *done;  // Ctl::scored (null: the merge waits on a stream event instead)
-    // fused merge (KC 4, K 16, single rank): the last B workgroups to finish merge one pod each
-    int32_t fuse_merge;
-    int32_t g_total;                 // workgroups of this launch
-    unsigned long long done_base;    // Ctl::scored before this launch
+    // device-side wait for commit(b-2): poll *wait_committed >= wait_target (null: the stream waits)
+    const unsigned long long *wait_committed;
+    unsigned long long wait_target;
+    int32_t *err;                    // device error word (4 = the wait timed out)
 };
 
 struct MergeArgs {
@@ -141,7 +142,22 @@ struct CommitArgs {
     XBuf *xout;             // nodes committed by this batch
     OutArgs out;
     int64_t *dbg;           // diagnostics only (KSCHED_COMMIT_STAMPS): per-phase cycle sums, else null
+    int64_t batch;          // this batch's index in the call (published to Ctl::committed when done)
 };
+
+// Commit(b) -> score(b+2) hand-off on the device: the committing wave drains its stores, writes back the
+// XCD L2 (agent release) and publishes Ctl::committed = b + 1; score(b+2) polls it instead of waiting
+// on a cross-queue stream event (~12 us per hand-off).  Call from ONE wave that
+// made every global store of the commit (the others made none).
+__device__ __forceinline__ void publish_committed(const CommitArgs &A) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 struct alignas(8) PodStage {
     int64_t rc, rm, rp;
@@ -184,15 +200,6 @@ __device__ __forceinline__ void plan_after_commit(const CommitArgs &A, bool trun
     *A.plan2 = nx;
 }
 
-// Lane-per-pod commit (k_commit_lp, B <= 64): touched slots <= previous batch's commits + this batch's.
-constexpr int kLpSlots = 128;
-constexpr int kLpThreads = 1024;  // prologue: 16 waves re-score the inherited slots; then wave 0 sequences
-constexpr size_t commit_lp_lds_bytes(int K) {
-    return kTouchHash * sizeof(int32_t) + kTouchFilterWords * sizeof(uint32_t) + kLpSlots * sizeof(int32_t) +
-           2 * 64 * sizeof(int32_t) + kLpSlots * sizeof(Touched) + (size_t)64 * (kLpSlots + 1) * sizeof(double) +
-           (size_t)64 * K * (sizeof(CandStage) + sizeof(double) + sizeof(int32_t));
-}
-static_assert(commit_lp_lds_bytes(16) <= 160 * 1024, "k_commit_lp LDS");
 constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
 
 // FailedScheduling diagnostics of a whole schedule call (ksched_explain.hip).
@@ -220,7 +227,7 @@ hipError_t explain_pod_at(const ExplainArgs &a, int64_t pod, int64_t *state, uin
 hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s);
 hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool fast53, const ExactArgs &a, int block,
                         bool cooperative, hipStream_t s);
-hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, const MergeArgs &m, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool fast53, const ScoreArgs &a, int pod_groups,
                              hipStream_t s);
 // one workgroup per pod: the score kernel's workgroup lists -> the pod's K-entry Rec list (C_in <= 256)
 hipError_t launch_merge_pod(int KC, int K, const MergeArgs &a, hipStream_t s);
@@ -229,7 +236,11 @@ hipError_t launch_commit(int K, int prio, int dom, bool lab, bool fast53, const 
                          hipStream_t s);
 constexpr int kSpcThreads = 512;  // speculative commit: wave 0 guesses and checks, 8 waves evaluate
 hipError_t launch_commit_spc(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
-hipError_t launch_commit_lp(int K, int prio, int dom, bool lab, bool fast53, const CommitArgs &a, hipStream_t s);
+hipError_t commit_spc_attributes(int K, int prio, int dom, bool lab, bool fast53, hipFuncAttributes *at, size_t *lds);
+// Can the batch's commit workgroup dispatch onto a CU that holds a score workgroup (VGPRs, LDS, wave
+// slots)?  Only then may score(b) be resident and poll for commit(b-2): otherwise the score grid
+// could occupy every CU while the commit it waits for never gets in.
+bool commit_fits_beside_score(int KC, int K, int B, bool spc, int prio, int dom, bool lab, bool fast53);
 constexpr int kNumReasons = 5;  // fit, Insufficient CPU, Insufficient Memory, Insufficient Pod, labels
 hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t rm, int64_t rp, uint64_t sel,
                           bool use_labels, uint8_t *reason, unsigned long long *counts, hipStream_t s);

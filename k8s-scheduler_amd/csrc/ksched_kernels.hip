@@ -231,6 +231,27 @@ __device__ __forceinline__ void score_topk_body(const ScoreArgs &A) {
     const int64_t G = gridDim.x;
     const int64_t NSC = G * kScoreWaves;
     const int64_t sub = (int64_t)blockIdx.x + G * wave;
+    if (A.wait_committed) {
+        // commit(b-2) published its plan for this batch, its commits (XBuf) and Ctl::committed with an
+        // agent release: one lane polls (relaxed, s_sleep), one agent acquire, then plain loads
+        __shared__ int s_late;
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = wall_clock64();
+            s_late = 0;
+            while (__hip_atomic_load(A.wait_committed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < A.wait_target) {
+                __builtin_amdgcn_s_sleep(1);
+                if (wall_clock64() - t0 > 200000000ull) {  // 2 s: report instead of spinning forever
+                    __hip_atomic_store(A.err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    s_late = 1;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (s_late) return;
+    }
     // Batch b-2's commits (<= 128 nodes, two per lane): the wave whose sub-chunk holds a node writes it
     // back to the row (for the next launches) and overlays it on what it reads in this launch, so no
     // separate apply kernel has to run between commit(b-2) and score(b).
@@ -572,34 +593,13 @@ __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
     merge_pod_body<KC, K>(A, blockIdx.x);
 }
 
-// Score kernel.  FUSE (KC 4, K 16, single rank): every workgroup publishes its lists (release) and
-// takes an arrival number from Ctl::scored; the last B arrivals wait for the rest (at most B - 1
-// workgroups, all already dispatched or dispatchable: no early-resident consumers) and merge one pod
-// each, so no merge kernel and no score -> merge queue hand-off exist.
-template <int KC, int PRIO, int DOM, bool LAB, bool F53, bool FUSE>
+// Score kernel (the merge waits on a stream event, or polls Ctl::scored when A.done is set).
 // <= 64 VGPRs (launch bound: 8 waves per SIMD): two score waves + two commit waves (190 VGPRs) must
 // fit one SIMD, or the single-workgroup commit cannot dispatch beside the score grid.
-__global__ __launch_bounds__(kScoreThreads, 8) void k_score_topk(ScoreArgs A, MergeArgs M) {
+template <int KC, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(kScoreThreads, 8) void k_score_topk(ScoreArgs A) {
     score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
-    if constexpr (FUSE) {
-        static_assert(kScoreThreads == kMergeThreads, "fused merge runs one pod per score workgroup");
-        __shared__ int s_arr;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            s_arr = (int)(__hip_atomic_fetch_add(A.done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - A.done_base);
-        }
-        __syncthreads();
-        const int first = A.g_total - A.B;
-        const int arr = s_arr;
-        if (arr < first) return;
-        wait_scored(A.done, A.done_base + (unsigned long long)A.g_total, M.err);
-        merge_pod_body<4, 16>(M, arr - first);
-    } else {
-        if (A.done) signal_scored(A.done);
-    }
+    if (A.done) signal_scored(A.done);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -958,6 +958,7 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
             if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
             plan_after_commit(A, false, cursor);
         }
+        publish_committed(A);
         return;
     }
     CommitCtx cx;
@@ -1055,6 +1056,7 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
         A.ctl->stats[2] += cx.placed;
         plan_after_commit(A, done < nb, p0 + done);
     }
+    publish_committed(A);
 }
 
 // Pipeline control at the start of a batched call: batch 0 starts at pod 0, batch 1 speculatively at B;
@@ -1064,6 +1066,7 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     ctl->cursor = 0; ctl->spec_next = 0; ctl->resync = 0;
     for (int i = 0; i < 5; ++i) ctl->stats[i] = 0;
     ctl->scored = 0;
+    ctl->committed = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;
     ctl->plan[0] = P > 0 ? 0 : -1;
     ctl->plan[1] = B < P ? B : -1;
@@ -1148,32 +1151,28 @@ hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStrea
     }
 }
 
-template <int KC, int PRIO, int DOM, bool LAB, bool F53, bool FUSE>
-hipError_t score_one(const ScoreArgs &a, const MergeArgs &m, int pod_groups, hipStream_t s) {
+template <int KC, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
     const size_t lds = score_lds_bytes(KC);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_score_topk<KC, PRIO, DOM, LAB, F53, FUSE>,
+        hipError_t e = hipFuncSetAttribute((const void *)k_score_topk<KC, PRIO, DOM, LAB, F53>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     dim3 grid((unsigned)(a.n_chunks / kScoreWaves), pod_groups);
-    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53, FUSE>), grid, dim3(kScoreThreads), lds, s, a, m);
+    hipLaunchKernelGGL((k_score_topk<KC, PRIO, DOM, LAB, F53>), grid, dim3(kScoreThreads), lds, s, a);
     return hipGetLastError();
 }
 
 template <int PRIO, int DOM, bool LAB, bool F53>
-hipError_t score_k(int KC, const ScoreArgs &a, const MergeArgs &m, int pg, hipStream_t s) {
-    if (a.fuse_merge) {
-        if (KC != 4 || pg != 1) return hipErrorInvalidValue;
-        return score_one<4, PRIO, DOM, LAB, F53, true>(a, m, pg, s);
-    }
+hipError_t score_k(int KC, const ScoreArgs &a, int pg, hipStream_t s) {
     switch (KC) {
-        case 2: return score_one<2, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
-        case 4: return score_one<4, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
-        case 8: return score_one<8, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
-        case 16: return score_one<16, PRIO, DOM, LAB, F53, false>(a, m, pg, s);
+        case 2: return score_one<2, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 4: return score_one<4, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 8: return score_one<8, PRIO, DOM, LAB, F53>(a, pg, s);
+        case 16: return score_one<16, PRIO, DOM, LAB, F53>(a, pg, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1230,6 +1229,57 @@ hipError_t commit_k(int K, const CommitArgs &a, size_t lds, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t score_attr_k(int KC, hipFuncAttributes *at) {
+    switch (KC) {
+        case 2: return hipFuncGetAttributes(at, (const void *)k_score_topk<2, PRIO, DOM, LAB, F53>);
+        case 4: return hipFuncGetAttributes(at, (const void *)k_score_topk<4, PRIO, DOM, LAB, F53>);
+        case 8: return hipFuncGetAttributes(at, (const void *)k_score_topk<8, PRIO, DOM, LAB, F53>);
+        case 16: return hipFuncGetAttributes(at, (const void *)k_score_topk<16, PRIO, DOM, LAB, F53>);
+        default: return hipErrorInvalidValue;
+    }
+}
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t commit_attr_one(hipFuncAttributes *at) {
+    return hipFuncGetAttributes(at, (const void *)k_commit<K, PRIO, DOM, LAB, F53>);
+}
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t commit_attr_k(int K, hipFuncAttributes *at) {
+    switch (K) {
+        case 4: return commit_attr_one<4, PRIO, DOM, LAB, F53>(at);
+        case 8: return commit_attr_one<8, PRIO, DOM, LAB, F53>(at);
+        case 16: return commit_attr_one<16, PRIO, DOM, LAB, F53>(at);
+        default: return hipErrorInvalidValue;
+    }
+}
+hipError_t score_attributes(int KC, int prio, int dom, bool lab, bool f53, hipFuncAttributes *at) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (score_attr_k<P_, D_, L_, F_>(KC, at)));
+}
+hipError_t seq_commit_attributes(int K, int prio, int dom, bool lab, bool f53, hipFuncAttributes *at) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (commit_attr_k<P_, D_, L_, F_>(K, at)));
+}
+int alloc_vgprs(int n) { return (n + 7) / 8 * 8; }
+}  // namespace
+
+bool commit_fits_beside_score(int KC, int K, int B, bool spc, int prio, int dom, bool lab, bool f53) {
+    hipFuncAttributes sa{}, ca{};
+    size_t commit_lds = 0;
+    if (score_attributes(KC, prio, dom, lab, f53, &sa) != hipSuccess) return false;
+    if (spc) {
+        if (commit_spc_attributes(K, prio, dom, lab, f53, &ca, &commit_lds) != hipSuccess) return false;
+    } else {
+        if (seq_commit_attributes(K, prio, dom, lab, f53, &ca) != hipSuccess) return false;
+        commit_lds = commit_lds_bytes(B, K);
+    }
+    const int score_waves_per_simd = kScoreThreads / 64 / 4;
+    const int commit_waves_per_simd = spc ? kSpcThreads / 64 / 4 : 1;
+    const int vgpr = score_waves_per_simd * alloc_vgprs(sa.numRegs) + commit_waves_per_simd * alloc_vgprs(ca.numRegs);
+    const size_t lds = sa.sharedSizeBytes + score_lds_bytes(KC) + ca.sharedSizeBytes + commit_lds;
+    const int waves = kScoreThreads / 64 + (spc ? kSpcThreads / 64 : 1);
+    return vgpr <= 512 && lds <= 160 * 1024 && waves <= 32;
+}
+
 hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_prep_nodes, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nodes, n);
@@ -1241,9 +1291,9 @@ hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool f53, const Ex
     KSCHED_DISPATCH(prio, dom, lab, f53, (exact_npt<P_, D_, L_, F_>(npt, a, block, coop, s)));
 }
 
-hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, const MergeArgs &m, int pod_groups,
+hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,
                              hipStream_t s) {
-    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(KC, a, m, pod_groups, s)));
+    KSCHED_DISPATCH(prio, dom, lab, f53, (score_k<P_, D_, L_, F_>(KC, a, pod_groups, s)));
 }
 
 hipError_t launch_merge(int KIN, int K, bool input_rec, bool final_stage, const MergeArgs &a, hipStream_t s) {
