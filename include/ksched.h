@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 1
+#define KSCHED_ABI_VERSION 2
 
 /* status codes */
 #define KSCHED_OK 0
@@ -92,7 +92,16 @@ typedef struct ksched_stats {
                               [1] merge, [2] commit, [3] collective (all-gather + rank merge) */
     int64_t kernel_launches[4]; /* number of timed batches (launch groups) behind kernel_ms */
     int64_t kernel_pairs[4];    /* pod-node pairs evaluated by the timed family-0 launches */
+    int64_t pipeline;           /* which device pipeline ran the last call: KSCHED_PIPE_* (ABI 2) */
 } ksched_stats;
+
+enum {
+    KSCHED_PIPE_NONE = 0,       /* no pods */
+    KSCHED_PIPE_EXACT = 1,      /* the exact persistent kernel, one pod at a time */
+    KSCHED_PIPE_STREAM = 2,     /* batched: score / merge / speculative commit kernels per batch, stream-linked */
+    KSCHED_PIPE_STREAM_SEQ = 3, /* batched with the sequential one-pod-at-a-time commit kernel */
+    KSCHED_PIPE_PERSISTENT = 4  /* batched single-rank: resident score grid + resident commit workgroup */
+};
 
 /* ---- lifecycle ---- */
 int ksched_abi_version(void);

@@ -108,26 +108,25 @@ __device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64
 
 }  // namespace
 
-// <= 192 VGPRs (amdgpu_num_vgpr counts half the unified gfx950 file): beside a resident score workgroup (two 64-VGPR waves per SIMD) the commit's two waves
-// per SIMD must fit the 512-entry file, or a score grid polling for this commit would never let it in.
-template <int K, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) void k_commit_spc(CommitArgs A) {
-    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+// One batch's ordered commit by the whole workgroup (kSpcThreads).  COH: the lists arrive from other
+// workgroups of a running persistent kernel (sc1 loads), and what the score workgroups read back --
+// the XBuf export, the next plans, the cursor -- leaves as sc1 stores (ksched_persist.hip).
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH>
+__device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int64_t p0 = *A.plan;
-    const int64_t cursor = A.ctl->cursor;
+    const int64_t p0 = load_i64<COH>(A.plan);
+    const int64_t cursor = load_i64<COH>(&A.ctl->cursor);
     if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
         // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
         if (wave == 0) {
             if (lane == 0) {
-                A.xout->count = 0;
-                if (p0 >= 0 && p0 < A.pods.p) A.ctl->stats[3] += 1;
-                plan_after_commit(A, false, cursor);
+                if (COH) st_coh(&A.xout->count, 0ull); else A.xout->count = 0;
+                if (p0 >= 0 && p0 < A.pods.p) add_i64<COH>(&A.ctl->stats[3], 1);
+                plan_after_commit<COH>(A, false, cursor);
             }
-            publish_committed(A);
+            publish_committed<COH>(A);
         }
         return;
     }
@@ -165,8 +164,8 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
     const int64_t rm = pj ? A.pods.rm[p0 + lane] : 0;
     const int64_t rp = pj ? A.pods.rp[p0 + lane] : 0;
     const uint64_t sel = (LAB && pj) ? A.pods.sel[p0 + lane] : 0;
-    const int64_t fc0v = (wave == 0 && pj) ? A.fc0[lane] : 0;
-    const int cut0 = (wave == 0 && pj) ? A.lists[(size_t)lane * K].pad : 0;
+    const int64_t fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
+    const int cut0 = (wave == 0 && pj) ? load_rec<COH>(A.lists + (size_t)lane * K).pad : 0;
 
     // ---- prologue (all waves) ----
     for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
@@ -177,16 +176,16 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
         double key = -__builtin_inf();
         int32_t idx = kNoIdx;
         if (j < nb) {
-            const Rec &r = A.lists[e];
+            const Rec r = load_rec<COH>(A.lists + e);
             if (r.valid) { key = r.key; idx = r.idx; }
         }
         m.LK[q * 64 + j] = key;
         m.LI[q * 64 + j] = idx;
         m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
     }
-    const int nin = A.xin->count;  // <= 64
+    const int nin = COH ? (int)(uint32_t)ld_coh(&A.xin->count) : A.xin->count;  // <= 64
     for (int e = tid; e < nin; e += kSpcThreads) {
-        const XRec &xi = A.xin->e[e];
+        const XRec xi = load_xrec<COH>(&A.xin->e[e]);
         SpcSlot &x = m.T[e];
         x.idx = xi.idx; x.mine = 0;
         for (int r = 0; r < 3; ++r) { x.s0[r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
@@ -315,7 +314,7 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
                 gg[u] = __builtin_amdgcn_readfirstlane(k < rce ? m.gn[k] : -1);
                 ss[u] = 0; ra0[u] = ra1[u] = ra2[u] = 0; rlab[u] = 0; rpr[u] = 0.f;
                 if (gg[u] >= 0) {
-                    const Rec &r = A.lists[(size_t)k * K + __builtin_amdgcn_readfirstlane(m.gq[k])];
+                    const Rec r = load_rec<COH>(A.lists + (size_t)k * K + __builtin_amdgcn_readfirstlane(m.gq[k]));
                     ss[u] = __builtin_amdgcn_readfirstlane(m.gs[k]);
                     ra0[u] = r.a[0]; ra1[u] = r.a[1]; ra2[u] = r.a[2]; rlab[u] = r.labels; rpr[u] = r.price;
                 }
@@ -472,7 +471,7 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
                         uint64_t lab;
                         float pr;
                         if (kf == 1) {  // first touch of list entry qf
-                            const Rec &r = A.lists[(size_t)f * K + qf];
+                            const Rec r = load_rec<COH>(A.lists + (size_t)f * K + qf);
                             b0 = r.a[0]; b1 = r.a[1]; b2 = r.a[2]; lab = r.labels; pr = r.price;
                             s = nT++;
                         } else {
@@ -546,28 +545,113 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
         const uint64_t mask = __ballot(mine);
         if (mine) {
             const SpcSlot &x = m.T[t];
-            XRec &o = A.xout->e[base + __popcll(mask & ((1ull << lane) - 1))];
+            XRec o;
             o.idx = x.idx; o.pad = 0;
             o.sb[0] = x.sb[0]; o.sb[1] = x.sb[1]; o.sb[2] = x.sb[2];
             o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
             o.labels = x.labels; o.price = x.price; o.pad2 = 0;
+            store_xrec<COH>(&A.xout->e[base + __popcll(mask & ((1ull << lane) - 1))], o);
         }
         base += __popcll(mask);
     }
     if (lane == 0) {
-        A.xout->count = base;
-        A.ctl->cursor = p0 + done;
-        A.ctl->stats[0] += 1;
-        A.ctl->stats[1] += (done < nb) ? 1 : 0;
-        A.ctl->stats[2] += placed;
-        plan_after_commit(A, done < nb, p0 + done);
+        if (COH) st_coh(&A.xout->count, (uint64_t)(uint32_t)base); else A.xout->count = base;
+        store_i64<COH>(&A.ctl->cursor, p0 + done);
+        add_i64<COH>(&A.ctl->stats[0], 1);
+        add_i64<COH>(&A.ctl->stats[1], (done < nb) ? 1 : 0);
+        add_i64<COH>(&A.ctl->stats[2], placed);
+        plan_after_commit<COH>(A, done < nb, p0 + done);
         if (A.dbg) {
             A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1;
             A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
             A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
         }
     }
-    publish_committed(A);  // wave 0 made every global store of this kernel
+    publish_committed<COH>(A);  // wave 0 made every global store of this batch
+}
+
+// <= 192 VGPRs (amdgpu_num_vgpr counts half the unified gfx950 file): beside a resident score
+// workgroup (two 64-VGPR waves per SIMD) the commit's two waves per SIMD must fit the 512-entry file,
+// or a score grid polling for this commit would never let it in.
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) void k_commit_spc(CommitArgs A) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    commit_spc_batch<K, PRIO, DOM, LAB, F53, false>(A, smem);
+}
+
+// ------------------------------------------------------------------------------------------------
+// The commit side of the persistent pipeline: ONE workgroup resident for the whole call, batch after
+// batch.  It waits for the B merges of an active batch (Ctl::merged, sc1 poll), commits it exactly as
+// k_commit_spc does (lists read with sc1 loads; export, plans and cursor left as sc1 stores) and
+// publishes Ctl::committed.  Once every pod is resolved it publishes a committed count no wait can
+// exceed, so every score workgroup still waiting can see the end.  Every wait is bounded (2 s).
+// It runs alone on the CU the score grid leaves free, so it is not capped below 256 VGPRs.
+// ------------------------------------------------------------------------------------------------
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
+    __builtin_amdgcn_s_setprio(3);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ int s_stop;
+    Ctl *ctl = P.ctl;
+    int64_t nact = 0;
+    int idle = 0;
+    for (int64_t b = 0;; ++b) {
+        const int64_t p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);  // written by this workgroup / k_ctl_init
+        if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
+            // pods remain but nothing is planned: a truncation re-plans within two batches, so this is a
+            // protocol error -- stop everyone instead of spinning
+            if (threadIdx.x == 0) {
+                atomicCAS(P.err, 0, 9);
+                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
+        if (p0 >= 0 && p0 < P.pods.p) {
+            idle = 0;
+            ++nact;
+            if (threadIdx.x == 0) {
+                const uint64_t t0 = wall_clock64();
+                s_stop = 0;
+                const int slot = (int)((nact - 1) % 4);
+                const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
+                while (__hip_atomic_load(&ctl->merged[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                    if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) { s_stop = 1; break; }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            if (s_stop) {
+                if (threadIdx.x == 0) {
+                    atomicCAS(P.err, 0, 5);
+                    __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                return;
+            }
+        }
+        if (threadIdx.x == 0) trace_at(P, b, 3);
+        CommitArgs ca{};
+        char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
+        ca.lists = reinterpret_cast<const Rec *>(lb);
+        ca.fc0 = reinterpret_cast<const int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
+        ca.pods = P.pods; ca.ctl = ctl; ca.B = P.B;
+        ca.plan = &ctl->plan[b % kPlanRing];
+        ca.plan1 = &ctl->plan[(b + 1) % kPlanRing];
+        ca.plan2 = &ctl->plan[(b + 2) % kPlanRing];
+        ca.xin = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes);
+        ca.xout = reinterpret_cast<XBuf *>(P.xring + (size_t)(b % 4) * P.xbuf_bytes);
+        ca.out = P.out;
+        ca.batch = b;
+        ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
+        commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem);
+        __syncthreads();
+        if (threadIdx.x == 0) trace_at(P, b, 4);
+        if ((int64_t)ld_coh(&ctl->cursor) >= P.pods.p) {
+            if (threadIdx.x == 0)
+                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+    }
 }
 
 namespace {
@@ -622,6 +706,36 @@ hipError_t spc_attr_k(int K, hipFuncAttributes *at, size_t *lds) {
     }
 }
 }  // namespace
+
+namespace {
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t persist_commit_one(const PersistArgs &a, hipStream_t s) {
+    static bool attr_set = false;
+    const size_t lds = spc_lds_bytes<K>();
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void *)k_persist_commit<K, PRIO, DOM, LAB, F53>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_persist_commit<K, PRIO, DOM, LAB, F53>), dim3(1), dim3(kSpcThreads), lds, s, a);
+    return hipGetLastError();
+}
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t persist_commit_k(int K, const PersistArgs &a, hipStream_t s) {
+    switch (K) {
+        case 4: return persist_commit_one<4, PRIO, DOM, LAB, F53>(a, s);
+        case 8: return persist_commit_one<8, PRIO, DOM, LAB, F53>(a, s);
+        case 16: return persist_commit_one<16, PRIO, DOM, LAB, F53>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+}  // namespace
+
+hipError_t launch_persist_commit(int K, int prio, int dom, bool lab, bool f53, const PersistArgs &a, hipStream_t s) {
+    if (a.B > 64) return hipErrorInvalidValue;
+    KSCHED_DISPATCH(prio, dom, lab, f53, (persist_commit_k<P_, D_, L_, F_>(K, a, s)));
+}
 
 hipError_t commit_spc_attributes(int K, int prio, int dom, bool lab, bool f53, hipFuncAttributes *at, size_t *lds) {
     KSCHED_DISPATCH(prio, dom, lab, f53, (spc_attr_k<P_, D_, L_, F_>(K, at, lds)));

@@ -18,6 +18,20 @@
 
 namespace ksched {
 
+// ---- coherent (sc1) 8-byte accesses: hand-offs between workgroups of persistent kernels ----------
+// MI355X_MICROARCH "valid forms", row 1: every store of the handed-off bytes an sc1 store (relaxed
+// agent-scope atomic = global_store ... sc1), drained (s_waitcnt vmcnt(0)) before ONE lane's flag /
+// counter update; every load of them an sc1 load, after the poll.  No fences, no L2 write-back.
+__device__ __forceinline__ uint64_t ld_coh(const void *p) {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(void *p, uint64_t v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coh_f64(const void *p) { return __longlong_as_double((long long)ld_coh(p)); }
+__device__ __forceinline__ void st_coh_f64(void *p, double v) { st_coh(p, (uint64_t)__double_as_longlong(v)); }
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 constexpr int kPrioResource = 0;
 constexpr int kPrioPrice = 1;
 constexpr int kDomAll = 0;
@@ -68,7 +82,44 @@ struct alignas(8) Rec {
 };
 static_assert(sizeof(Rec) == 56, "Rec layout");
 
+// Rec loads / stores, plain or coherent (COH: 8-byte sc1 accesses, Rec words w0..w6).
+template <bool COH>
+__device__ __forceinline__ Rec load_rec(const Rec *p) {
+    if constexpr (!COH) {
+        return *p;
+    } else {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
+        Rec r;
+        const uint64_t w1 = ld_coh(w + 1), w6 = ld_coh(w + 6);
+        r.key = __longlong_as_double((long long)ld_coh(w));
+        r.idx = (int32_t)(uint32_t)w1; r.valid = (int32_t)(uint32_t)(w1 >> 32);
+        r.a[0] = (int64_t)ld_coh(w + 2); r.a[1] = (int64_t)ld_coh(w + 3); r.a[2] = (int64_t)ld_coh(w + 4);
+        r.labels = ld_coh(w + 5);
+        r.price = __uint_as_float((uint32_t)w6); r.pad = (int32_t)(uint32_t)(w6 >> 32);
+        return r;
+    }
+}
+template <bool COH>
+__device__ __forceinline__ void store_rec(Rec *p, const Rec &r) {
+    if constexpr (!COH) {
+        *p = r;
+    } else {
+        uint64_t *w = reinterpret_cast<uint64_t *>(p);
+        st_coh(w, (uint64_t)__double_as_longlong(r.key));
+        st_coh(w + 1, (uint64_t)(uint32_t)r.idx | ((uint64_t)(uint32_t)r.valid << 32));
+        st_coh(w + 2, (uint64_t)r.a[0]); st_coh(w + 3, (uint64_t)r.a[1]); st_coh(w + 4, (uint64_t)r.a[2]);
+        st_coh(w + 5, r.labels);
+        st_coh(w + 6, (uint64_t)__float_as_uint(r.price) | ((uint64_t)(uint32_t)r.pad << 32));
+    }
+}
+template <bool COH>
+__device__ __forceinline__ int64_t load_i64(const int64_t *p) { return COH ? (int64_t)ld_coh(p) : *p; }
+template <bool COH>
+__device__ __forceinline__ void store_i64(int64_t *p, int64_t v) { if (COH) st_coh(p, (uint64_t)v); else *p = v; }
+
 __host__ __device__ inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+
+
 
 // (key desc, idx asc): the deterministic restatement of the reference's map-order argmax.
 __device__ __forceinline__ bool better(double ka, int32_t ia, double kb, int32_t ib) {

@@ -115,6 +115,13 @@ struct ksched_ctx {
     size_t xws_bytes = 0;
     void *d_xbuf = nullptr;      // counts + NO_FIT pod list, or one pod's state + counts
     size_t xbuf_bytes = 0;
+    // persistent single-rank pipeline (ksched_persist.hip)
+    void *d_pws = nullptr;       // per-workgroup part lists + counts
+    uint64_t *d_trace = nullptr;  // KSCHED_PERSIST_TRACE: per-batch wall-clock stamps
+    int64_t trace_cap = 0;
+    size_t pws_bytes = 0;
+    bool persist_stats = false;  // stats come from the Ctl copy queued behind the run
+    int64_t persist_B = 0;
 };
 
 namespace {
@@ -464,6 +471,118 @@ int enqueue_batched(ksched_ctx *c) {
     return KSCHED_OK;
 }
 
+// Single-rank batched mode as two resident kernels (ksched_persist.hip): no per-batch launches, no
+// stream events, node rows in LDS.  Returns 1 (not taken) when the configuration does not fit it --
+// multi-rank, a sequential commit (batch > 64), chunk lists > 8, or rows that do not fit in LDS --
+// and the stream pipeline runs instead.
+// KSCHED_PERSIST_TRACE=1: mean per-batch phase times of the last persistent run, to stderr (us)
+void print_persist_trace(ksched_ctx *c) {
+    std::vector<uint64_t> t((size_t)c->trace_cap * kTraceCols);
+    if (hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
+    double sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t cnt = 0, first = -1, last = -1;
+    for (int64_t b = 2; b < c->trace_cap; ++b) {
+        if (!at(b, 0) || !at(b, 1) || !at(b, 2) || !at(b, 3) || !at(b, 4) || !at(b - 2, 4)) continue;
+        if (first < 0) first = b;
+        last = b;
+        ++cnt;
+        sum[0] += (double)(int64_t)(at(b, 0) - at(b - 2, 4));  // commit(b-2) end -> score(b) start
+        sum[1] += (double)(int64_t)(at(b, 1) - at(b, 0));      // score (WG 0 start -> last arrival)
+        sum[2] += (double)(int64_t)(at(b, 2) - at(b, 1));      // merge
+        sum[3] += (double)(int64_t)(at(b, 3) - at(b, 2));      // last merge -> commit start
+        sum[4] += (double)(int64_t)(at(b, 4) - at(b, 3));      // commit
+        sum[5] += (double)(int64_t)(at(b, 3) - at(b - 1, 4));  // commit(b-1) end -> commit(b) start
+        sum[6] += (double)(int64_t)(at(b, 6) - at(b - 2, 4));  // WG 0: commit(b-2) end -> its poll returns
+        sum[7] += (double)(int64_t)(at(b, 0) - at(b, 6));      // WG 0: plan loads + XBuf apply
+        sum[8] += (double)(int64_t)(at(b, 5) - at(b, 0));      // WG 0: score + fold + list stores
+        sum[9] += (double)(int64_t)(at(b, 7) - at(b, 1));      // last arrival -> merger past its poll
+    }
+    if (!cnt) return;
+    const double us = 0.01 / (double)cnt;  // 100 MHz ticks -> us, mean
+    fprintf(stderr,
+            "persist trace: %lld batches, period %.2f us | to-score %.2f score %.2f merge %.2f to-commit %.2f "
+            "commit %.2f commit-gap %.2f | wg0: poll %.2f apply %.2f score %.2f | merger poll %.2f\n",
+            (long long)cnt, 0.01 * (double)(int64_t)(at(last, 4) - at(first, 4)) / (double)std::max<int64_t>(1, last - first),
+            sum[0] * us, sum[1] * us, sum[2] * us, sum[3] * us, sum[4] * us, sum[5] * us, sum[6] * us, sum[7] * us,
+            sum[8] * us, sum[9] * us);
+}
+
+constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
+
+int enqueue_persistent(ksched_ctx *c) {
+    if (env_int("KSCHED_PERSIST", 1) == 0) return 1;
+    if (c->comm || c->group || c->o.nranks > 1 || c->o.node_offset != 0) return 1;
+    const int K = c->K, KC = c->KC, B = c->B;
+    if (B > 64 || KC > 8 || (c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL)) return 1;
+    const int64_t n = c->n_local;
+    // workgroups of a launch go round-robin to the 8 XCDs (32 CUs each), so the grid must leave one CU
+    // free on EVERY XCD for the commit workgroup to be guaranteed a place: G <= CUs - 8 (measured: with
+    // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts)
+    const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - kXcds));
+    const int G = (int)std::max<int64_t>(B, std::min<int64_t>(gcap, (n + 15) / 16));
+    if (G < B || G > c->cus - kXcds) return 1;
+    const int R = (int)((n + G - 1) / G);
+    const size_t lds = persist_score_lds(KC, R);
+    if (lds == 0) return 1;
+    // workspace: part lists [2][B][G][KC] + counts [2][B][G], list ring 4 x (B*K Rec + B fc), XBuf ring
+    const size_t part_b = align_up((size_t)2 * B * G * KC * sizeof(Cand), 256);
+    const size_t cnt_b = align_up((size_t)2 * B * G * sizeof(int64_t), 256);
+    const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
+    const size_t xb = align_up(xbuf_bytes(B), 256);
+    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb;
+    if (c->pws_bytes < need) {
+        if (c->d_pws) hipFree(c->d_pws); hipFree(c->d_trace);
+        c->d_pws = nullptr;
+        c->pws_bytes = 0;
+        HIPCHK(c, hipMalloc(&c->d_pws, need));
+        c->pws_bytes = need;
+    }
+    char *w = static_cast<char *>(c->d_pws);
+    PersistArgs a{};
+    a.nodes = c->d_nodes; a.n_local = n;
+    a.pods = PodArgs{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
+    a.ctl = reinterpret_cast<Ctl *>(c->d_cursor);
+    a.B = B; a.G = G; a.rows_per_wg = R;
+    a.part = reinterpret_cast<Cand *>(w);
+    a.part_cnt = reinterpret_cast<int64_t *>(w + part_b);
+    a.lring = w + part_b + cnt_b;
+    a.lists_bytes = (int64_t)lists_b;
+    a.xring = a.lring + 4 * lists_b;
+    a.xbuf_bytes = (int64_t)xb;
+    a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
+    a.err = c->d_err;
+    a.timeout_ticks = 200000000;  // 2 s of the 100 MHz wall clock
+    if (env_int("KSCHED_PERSIST_TRACE", 0)) {
+        const int64_t cap = 4 * (c->p / B) + 64;
+        if (c->trace_cap < cap) {
+            if (c->d_trace) hipFree(c->d_trace);
+            c->d_trace = nullptr;
+            c->trace_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_trace, (size_t)cap * kTraceCols * 8));
+            c->trace_cap = cap;
+        }
+        HIPCHK(c, hipMemsetAsync(c->d_trace, 0, (size_t)c->trace_cap * kTraceCols * 8, c->stream));
+        a.trace = c->d_trace;
+        a.trace_cap = c->trace_cap;
+    }
+    hipStream_t sS = c->stream, sC = c->stream2;
+    HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, sS));
+    for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
+    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit stream starts after the initialisation
+    HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
+    const hipError_t e = launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC);
+    if (e == hipErrorInvalidValue) return 1;  // does not fit after all: the stream pipeline runs
+    if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("launch_persist: ") + hipGetErrorString(e));
+    HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));  // the run's end event on stream S covers the commit
+    HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
+    HIPCHK(c, hipMemcpyAsync(c->h_cursor, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, sS));
+    c->persist_stats = true;
+    c->persist_B = B;
+    c->run_batches = 0;
+    return KSCHED_OK;
+}
+
 int enqueue_exact(ksched_ctx *c) {
     if (c->o.nranks > 1) return fail(c, KSCHED_E_INVALID, "exact mode is single-GPU; use batched mode across ranks");
     const int64_t n = c->n_local;
@@ -595,7 +714,7 @@ int ksched_destroy(ksched_ctx *c) {
     }
     for (int i = 0; i < 2; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
-    hipFree(c->d_xws); hipFree(c->d_xbuf);
+    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
     delete c;
@@ -950,7 +1069,19 @@ int ksched_run(ksched_ctx *c) {
     if (c->p > 0) {
         int mode = c->o.mode;
         if (mode == KSCHED_MODE_AUTO) mode = c->o.nranks > 1 ? KSCHED_MODE_BATCHED : KSCHED_MODE_EXACT;
-        r = mode == KSCHED_MODE_EXACT ? enqueue_exact(c) : enqueue_batched(c);
+        c->persist_stats = false;
+        if (mode == KSCHED_MODE_EXACT) {
+            r = enqueue_exact(c);
+            c->st.pipeline = KSCHED_PIPE_EXACT;
+        } else {
+            r = enqueue_persistent(c);
+            c->st.pipeline = KSCHED_PIPE_PERSISTENT;
+            if (r == 1) {  // not eligible: the stream pipeline
+                r = enqueue_batched(c);
+                c->st.pipeline = c->B > 64 || c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL ? KSCHED_PIPE_STREAM_SEQ
+                                                                                          : KSCHED_PIPE_STREAM;
+            }
+        }
     }
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->running = r == KSCHED_OK;
@@ -979,8 +1110,31 @@ int ksched_sync(ksched_ctx *c) {
         }
         c->timed.clear();
     }
+    if (c->persist_stats && c->d_trace && env_int("KSCHED_PERSIST_TRACE", 0)) print_persist_trace(c);
+    if (c->persist_stats) {
+        const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+        c->st.batches = h->stats[0];
+        c->st.truncations = h->stats[1];
+        c->st.placed = h->stats[2];
+        c->st.pair_evals = (h->stats[0] + h->stats[3]) * c->persist_B * c->n_local;
+        c->persist_stats = false;
+    }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (e >= 5 && e <= 9) {
+        hipMemset(c->d_err, 0, sizeof(int32_t));
+        static const char *what[] = {"the commit's wait for the merges", "a score workgroup's wait for commit(b-2)",
+                                     "a merger's wait for the score workgroups", "the score grid's plan (idle)",
+                                     "the commit's plan (idle)"};
+        const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+        char buf[320];
+        snprintf(buf, sizeof buf,
+                 "persistent pipeline: %s timed out (committed %llu, arrive %llu/%llu/%llu/%llu, merged "
+                 "%llu/%llu/%llu/%llu, cursor %lld)",
+                 what[e - 5], h->committed, h->arrive[0], h->arrive[1], h->arrive[2], h->arrive[3], h->merged[0],
+                 h->merged[1], h->merged[2], h->merged[3], (long long)h->cursor);
+        return fail(c, KSCHED_E_DEVICE, buf);
+    }
     if (e == 2 || e == 4) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
         return fail(c, KSCHED_E_DEVICE, e == 2 ? "batched mode: the merge's wait for the score workgroups timed out"

@@ -44,6 +44,40 @@ struct alignas(8) XRec {
 };
 static_assert(sizeof(XRec) == 72, "XRec layout");
 
+template <bool COH>
+__device__ __forceinline__ XRec load_xrec(const XRec *p) {
+    if constexpr (!COH) {
+        return *p;
+    } else {
+        const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
+        XRec o;
+        const uint64_t w0 = ld_coh(w), w8 = ld_coh(w + 8);
+        o.idx = (int32_t)(uint32_t)w0; o.pad = (int32_t)(uint32_t)(w0 >> 32);
+        for (int r = 0; r < 3; ++r) { o.sb[r] = (int64_t)ld_coh(w + 1 + r); o.cur[r] = (int64_t)ld_coh(w + 4 + r); }
+        o.labels = ld_coh(w + 7);
+        o.price = __uint_as_float((uint32_t)w8); o.pad2 = (int32_t)(uint32_t)(w8 >> 32);
+        return o;
+    }
+}
+
+template <bool COH>
+__device__ __forceinline__ void add_i64(int64_t *p, int64_t v) {
+    if (COH) st_coh(p, (uint64_t)((int64_t)ld_coh(p) + v)); else *p += v;
+}
+
+template <bool COH>
+__device__ __forceinline__ void store_xrec(XRec *p, const XRec &o) {
+    if constexpr (!COH) {
+        *p = o;
+    } else {
+        uint64_t *w = reinterpret_cast<uint64_t *>(p);
+        st_coh(w, (uint64_t)(uint32_t)o.idx | ((uint64_t)(uint32_t)o.pad << 32));
+        for (int r = 0; r < 3; ++r) { st_coh(w + 1 + r, (uint64_t)o.sb[r]); st_coh(w + 4 + r, (uint64_t)o.cur[r]); }
+        st_coh(w + 7, o.labels);
+        st_coh(w + 8, (uint64_t)__float_as_uint(o.price) | ((uint64_t)(uint32_t)o.pad2 << 32));
+    }
+}
+
 struct alignas(8) XBuf {
     int32_t count;
     int32_t pad;
@@ -61,6 +95,13 @@ struct alignas(8) Ctl {
     int64_t plan[kPlanRing];
     unsigned long long scored;     // score workgroups finished this call (device hand-off to the merge)
     unsigned long long committed;  // batches committed this call: commit(b) publishes b + 1 (release)
+    // persistent pipeline (ksched_persist.hip)
+    // per active batch a (counted identically by every workgroup), slot a % 4 -- a workgroup can run one
+    // batch ahead of the slowest, so one shared counter would mix batches; four slots cannot (batch
+    // a + 4 waits for commit(a + 2), which waited for every merge of a + 2)
+    unsigned long long arrive[4];  // score workgroups done with active batch a: G per use of the slot
+    unsigned long long merged[4];  // merger workgroups done with active batch a: B per use of the slot
+    int64_t cursor_at[kPlanRing];  // cursor right after commit(b), slot b % kPlanRing
 };
 
 struct PodArgs {
@@ -143,17 +184,23 @@ struct CommitArgs {
     OutArgs out;
     int64_t *dbg;           // diagnostics only (KSCHED_COMMIT_STAMPS): per-phase cycle sums, else null
     int64_t batch;          // this batch's index in the call (published to Ctl::committed when done)
+    int64_t *cursor_at;     // persistent pipeline: &Ctl::cursor_at[batch % kPlanRing] (else null)
 };
 
 // Commit(b) -> score(b+2) hand-off on the device: the committing wave drains its stores, writes back the
 // XCD L2 (agent release) and publishes Ctl::committed = b + 1; score(b+2) polls it instead of waiting
 // on a cross-queue stream event (~12 us per hand-off).  Call from ONE wave that
 // made every global store of the commit (the others made none).
+// COH (persistent pipeline): every handed-off store was an sc1 store, so no L2 write-back is needed.
+template <bool COH = false>
 __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
+    if ((threadIdx.x & 63) == 0 && A.cursor_at) st_coh(A.cursor_at, ld_coh(&A.ctl->cursor));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((threadIdx.x & 63) == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (!COH) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __hip_atomic_store(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -193,11 +240,12 @@ constexpr size_t commit_lds_bytes(int B, int K) {
 // Speculative planning, done by the commit of batch k for batch k+2 (stream order makes plan(k+2)
 // visible to score(k+2), which waits for commit(k)): after a truncation restart at the committed
 // frontier, otherwise continue one batch after plan(k+1).  -1 = past the last pod.
+template <bool COH = false>
 __device__ __forceinline__ void plan_after_commit(const CommitArgs &A, bool truncated, int64_t cursor) {
-    const int64_t n1 = *A.plan1;
+    const int64_t n1 = load_i64<COH>(A.plan1);
     int64_t nx = truncated ? cursor : (n1 < 0 ? -1 : n1 + A.B);
     if (nx >= A.pods.p) nx = -1;
-    *A.plan2 = nx;
+    store_i64<COH>(A.plan2, nx);
 }
 
 constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
@@ -247,6 +295,41 @@ hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t r
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
 hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s);
+
+// ---- persistent single-rank pipeline (ksched_persist.hip) -------------------------------------
+// One score grid of G workgroups (one per CU, the WG's node rows resident in LDS for the whole call)
+// and one resident commit workgroup, joined by device counters in Ctl instead of launches and stream
+// events: score(b) waits for commit(b-2) (Ctl::committed), the last B score workgroups to finish batch
+// b merge one pod each (Ctl::arrive), commit(b) waits for the B merges (Ctl::merged).
+struct PersistArgs {
+    NodeRec *nodes;
+    int64_t n_local;
+    PodArgs pods;
+    Ctl *ctl;
+    int32_t B, G, rows_per_wg;
+    Cand *part;             // [2][B][G][KC]
+    int64_t *part_cnt;      // [2][B][G]
+    char *lring;            // 4 x {Rec [B][K]; int64 fc[B]}
+    int64_t lists_bytes;
+    char *xring;            // 4 XBufs + the permanently empty one (slot 4)
+    int64_t xbuf_bytes;
+    OutArgs out;
+    int32_t *err;           // device error word (5..9 = a persistent wait timed out)
+    int64_t timeout_ticks;
+    // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
+    uint64_t *trace;
+    int64_t trace_cap;
+};
+// trace columns: score start (WG 0 past its wait), last arrival, last merge done, commit start, commit end
+constexpr int kTraceCols = 8;
+__device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
+    if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
+}
+hipError_t launch_persist_commit(int K, int prio, int dom, bool lab, bool fast53, const PersistArgs &a, hipStream_t s);
+// bytes of dynamic LDS the score grid needs (0: the rows do not fit -> use the stream pipeline)
+size_t persist_score_lds(int KC, int rows_per_wg);
+hipError_t launch_persist(int KC, int K, int prio, int dom, bool lab, bool fast53, const PersistArgs &a, size_t lds,
+                          hipStream_t score_stream, hipStream_t commit_stream);
 hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s);
 // diagnostics: qdiv(a, b, recip(b)) against the native a / b, bit for bit
 hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,

@@ -1,0 +1,229 @@
+// ksched_merge.h -- device code shared by the stream pipeline (ksched_kernels.hip) and the persistent
+// pipeline (ksched_persist.hip): per-lane sorted top-K insert and the per-pod rank merge of the score
+// workgroups' lists.
+#pragma once
+
+#include "ksched_kernels.h"
+
+namespace ksched {
+
+template <int KC>
+__device__ __forceinline__ void list_insert_ordered(double (&key)[KC], int32_t (&idx)[KC], double ck, int32_t ci) {
+    bool moved = false;  // once placed, every later entry shifts down one slot
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+        const bool sw = moved || better(ck, ci, key[q], idx[q]);
+        moved = sw;
+        const double tk = key[q];
+        const int32_t ti = idx[q];
+        key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+        ck = sw ? tk : ck; ci = sw ? ti : ci;
+    }
+}
+
+// Consumer side: one relaxed (sc1) poll with s_sleep, one agent acquire, drain, workgroup barrier.  A
+// wall-clock timeout (2 s) sets the device error word instead of spinning forever.
+__device__ __forceinline__ void wait_scored(const unsigned long long *ctr, unsigned long long target, int32_t *err) {
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > 200000000ull) {
+                if (err) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Merge of one pod's workgroup lists (C_in <= 512 lists of KC entries, cut when full) into its K-entry
+// Rec list: one 512-thread workgroup per pod, thread = list.  Selection by RANK, every compare
+// independent (broadcast LDS reads of order-preserving 64-bit key codes; no serial rounds):
+//   1. each list head is ranked within its wave; the K best heads of each wave survive;
+//   2. the <= 8K survivors are ranked against each other; the K best heads' lists are kept -- every
+//      entry of the pod's top K lies in one of them (K better heads exist for any entry outside them);
+//   3. the kept lists' K*KC entries are ranked against each other; rank < K is the output position.
+// Exact prefix: the result keeps only entries ranking at or above the best cutoff (the last entry of
+// every cut input list) and is cut (flag in entry 0's pad) when any input was cut or entries were left
+// over.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb, int32_t ib) {
+    return ca > cb || (ca == cb && ia < ib);
+}
+
+template <int KC, int K, bool COH = false>
+__device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    constexpr int W = kMergeThreads / 64;
+    __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
+    __shared__ int32_t s_idx[kMergeThreads][KC];
+    __shared__ uint64_t s_ccode[W * K];             // surviving heads
+    __shared__ int32_t s_cidx[W * K], s_clist[W * K];
+    __shared__ int32_t s_keep[K];                   // list of global head rank g
+    __shared__ uint64_t s_ecode[K * KC];            // the kept lists' entries
+    __shared__ int32_t s_eidx[K * KC];
+    __shared__ uint64_t s_ocode[K];
+    __shared__ int32_t s_oidx[K];
+    __shared__ uint64_t s_wck[W];
+    __shared__ int32_t s_wci[W], s_wcut[W], s_wnv[W];
+    __shared__ int64_t s_wcnt[W];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const bool dbg = A.dbg != nullptr;
+    uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
+    const int64_t p0 = load_i64<COH>(A.cursor);
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // workgroup-uniform
+    if (A.wait_ctr) wait_scored(A.wait_ctr, A.wait_target, A.err);
+    const bool has = tid < A.C_in;
+    uint64_t code[KC];
+    int32_t idx[KC];
+    int n = 0;
+    int64_t cnt = 0;
+    {
+        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? tid : 0)) * KC;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            int32_t x;
+            double kq;
+            if (COH) {
+                x = has ? (int32_t)(uint32_t)ld_coh(&src[q].idx) : kNoIdx;
+                kq = has ? ld_coh_f64(&src[q].key) : 0.0;
+            } else {
+                x = has ? src[q].idx : kNoIdx;
+                kq = has ? src[q].key : 0.0;
+            }
+            idx[q] = x;
+            code[q] = x == kNoIdx ? 0ull : key_code(kq);
+            n += x != kNoIdx;
+        }
+        if (has) cnt = load_i64<COH>(A.in_cnt + (size_t)b * A.C_in + tid);
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { s_code[tid][q] = code[q]; s_idx[tid][q] = idx[q]; }
+    if (tid < W * K) { s_ccode[tid] = 0ull; s_cidx[tid] = kNoIdx; }  // empty survivor slots never rank
+    if (dbg) { asm volatile("" ::"v"(code[0]), "v"(cnt)); ts[1] = __builtin_amdgcn_s_memtime(); }
+    // wave partials: best cutoff (last entry of a full list), count, cut flag
+    {
+        const bool cut = n == KC;
+        uint64_t ck = cut ? code[KC - 1] : 0ull;
+        int32_t ci = cut ? idx[KC - 1] : kNoIdx;
+        const uint64_t bc = wave_max_u64(ck);
+        const int32_t bi = wave_min_i32((ck == bc && ci != kNoIdx) ? ci : kNoIdx);
+        const int64_t wc = wave_sum_i64(cnt);
+        const bool wcut = __ballot(cut) != 0;
+        const int nv = __popcll(__ballot(idx[0] != kNoIdx));
+        if (lane == 0) { s_wck[wave] = bc; s_wci[wave] = bi; s_wcut[wave] = wcut; s_wcnt[wave] = wc; s_wnv[wave] = nv; }
+    }
+    __syncthreads();
+    // 1. rank each head within its wave (broadcast reads, independent compares)
+    {
+        int rank = 0;
+        const int base = wave * 64;
+#pragma unroll 16
+        for (int t = 0; t < 64; ++t)
+            rank += code_better(s_code[base + t][0], s_idx[base + t][0], code[0], idx[0]) ? 1 : 0;
+        if (idx[0] != kNoIdx && rank < K) {
+            s_ccode[wave * K + rank] = code[0];
+            s_cidx[wave * K + rank] = idx[0];
+            s_clist[wave * K + rank] = tid;
+        }
+    }
+    if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
+    // 2. rank the survivors against each other
+    const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
+    int ntot = 0;  // valid heads in total (survivors: the first min(K, nv) slots of each wave)
+    for (int w = 0; w < nw; ++w) ntot += s_wnv[w];
+    if (tid < nw * K) {
+        const int w = tid / K, p = tid % K;
+        const int nvw = s_wnv[w] < K ? s_wnv[w] : K;
+        if (p < nvw) {
+            const uint64_t mc = s_ccode[tid];
+            const int32_t mi = s_cidx[tid];
+            int g = 0;
+#pragma unroll 16
+            for (int c = 0; c < W * K; ++c) g += code_better(s_ccode[c], s_cidx[c], mc, mi) ? 1 : 0;
+            if (g < K) s_keep[g] = s_clist[tid];
+        }
+    }
+    if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    // 3. gather the kept lists' entries (empty slots never rank), then rank them against each other
+    const int nkeep = ntot < K ? ntot : K;
+    const int ne = nkeep * KC;
+    if (tid < K * KC) {
+        const bool in = tid < ne;
+        const int l = in ? s_keep[tid / KC] : 0;
+        s_ecode[tid] = in ? s_code[l][tid % KC] : 0ull;
+        s_eidx[tid] = in ? s_idx[l][tid % KC] : kNoIdx;
+    }
+    __syncthreads();
+    int nvalid = 0;
+    if (tid < ne) {
+        const uint64_t mc = s_ecode[tid];
+        const int32_t mi = s_eidx[tid];
+        if (mi != kNoIdx) {
+            int r = 0;
+#pragma unroll 16
+            for (int e = 0; e < K * KC; ++e) r += code_better(s_ecode[e], s_eidx[e], mc, mi) ? 1 : 0;
+            if (r < K) { s_ocode[r] = mc; s_oidx[r] = mi; }
+        }
+    }
+    if (wave == 0) {
+        int cntv = 0;
+        for (int e0 = 0; e0 < K * KC; e0 += 64) {
+            const int e = e0 + lane;
+            cntv += __popcll(__ballot(e < K * KC && s_eidx[e < K * KC ? e : 0] != kNoIdx));
+        }
+        nvalid = cntv;
+    }
+    if (dbg) ts[5] = __builtin_amdgcn_s_memtime();
+    __syncthreads();
+    if (wave != 0) return;
+    uint64_t gk = 0ull;
+    int32_t gi = kNoIdx;
+    bool gcut = false;
+    int64_t gcnt = 0;
+    for (int w = 0; w < nw; ++w) {
+        if (s_wci[w] != kNoIdx && (gi == kNoIdx || code_better(s_wck[w], s_wci[w], gk, gi))) { gk = s_wck[w]; gi = s_wci[w]; }
+        gcut = gcut || s_wcut[w] != 0;
+        gcnt += s_wcnt[w];
+    }
+    const int nout = nvalid < K ? nvalid : K;
+    // lists outside the kept K, or entries beyond K, remain: the output is cut
+    const bool left = ntot > nkeep || nvalid > K;
+    const int32_t cut_out = (gcut || left) ? 1 : 0;
+    if (lane < K) {
+        Rec r{};
+        const uint64_t mc = s_ocode[lane < nout ? lane : 0];
+        const int32_t mi = s_oidx[lane < nout ? lane : 0];
+        const bool ok = lane < nout && !(gi != kNoIdx && code_better(gk, gi, mc, mi));
+        if (ok) {
+            const NodeRec &nd = A.nodes[mi - A.node_offset];
+            const uint64_t u = (mc >> 63) ? (mc & 0x7fffffffffffffffull) : ~mc;  // inverse of key_code
+            r.key = __longlong_as_double((long long)u); r.idx = mi; r.valid = 1;
+            r.a[0] = load_i64<COH>(&nd.a[0]); r.a[1] = load_i64<COH>(&nd.a[1]); r.a[2] = load_i64<COH>(&nd.a[2]);
+            r.labels = nd.labels; r.price = nd.price;  // never written during a call
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        r.pad = lane == 0 ? cut_out : 0;
+        store_rec<COH>(A.out_rec + (size_t)b * K + lane, r);
+    }
+    if (lane == 0) store_i64<COH>(A.out_fc + b, gcnt);
+    if (dbg && lane == 0) {
+        ts[6] = __builtin_amdgcn_s_memtime();
+        for (int k = 1; k < 7; ++k) atomicAdd((unsigned long long *)&A.dbg[k - 1], (unsigned long long)(ts[k] - ts[k - 1]));
+        atomicAdd((unsigned long long *)&A.dbg[7], 1ull);
+    }
+}
+
+
+}  // namespace ksched

@@ -48,7 +48,8 @@ class Opts(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("pods", C.c_int64), ("placed", C.c_int64), ("batches", C.c_int64), ("truncations", C.c_int64),
                 ("pair_evals", C.c_int64), ("device_ms", C.c_double), ("kernel_ms", C.c_double * 4),
-                ("kernel_launches", C.c_int64 * 4), ("kernel_pairs", C.c_int64 * 4)]
+                ("kernel_launches", C.c_int64 * 4), ("kernel_pairs", C.c_int64 * 4),
+                ("pipeline", C.c_int64)]
 
 
 class KschedError(RuntimeError):
@@ -116,7 +117,7 @@ def lib():
             fn = getattr(lb, name)
             fn.restype = res
             fn.argtypes = args
-        if lb.ksched_abi_version() != 1:
+        if lb.ksched_abi_version() != 2:
             raise ImportError("libksched ABI version mismatch")
         _lib = lb
     return _lib

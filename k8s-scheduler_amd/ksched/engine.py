@@ -17,6 +17,9 @@ import numpy as np
 
 from . import _lib as L
 
+# ksched_stats.pipeline (include/ksched.h KSCHED_PIPE_*)
+PIPELINES = {0: "none", 1: "exact", 2: "stream", 3: "stream-sequential", 4: "persistent"}
+
 
 def _i64(a):
     return np.ascontiguousarray(a, dtype=np.int64)
@@ -185,7 +188,8 @@ class Engine:
         self._chk(L.lib().ksched_get_stats(self._ctx, C.byref(s)), "get_stats")
         return dict(pods=s.pods, placed=s.placed, batches=s.batches, truncations=s.truncations,
                     pair_evals=s.pair_evals, device_ms=s.device_ms, kernel_ms=list(s.kernel_ms),
-                    kernel_launches=list(s.kernel_launches), kernel_pairs=list(s.kernel_pairs))
+                    kernel_launches=list(s.kernel_launches), kernel_pairs=list(s.kernel_pairs),
+                    pipeline=PIPELINES.get(int(s.pipeline), str(int(s.pipeline))))
 
     def set_timing(self, on: bool, every: int = 0):
         """Sampled per-kernel HIP-event timing for the following calls (every: one batch in N)."""

@@ -267,44 +267,38 @@ def test_sharded_engine_helper_world1(gpu_available, oracle_mod):
     assert_same((oi, os_, of, st), oracle_mod.schedule(cl), "sharded-helper")
 
 
-@pytest.mark.parametrize("env", ["KSCHED_DEVICE_HANDOFF", "KSCHED_SCORE_EVENT"])
+@pytest.mark.parametrize("env", [{"KSCHED_PERSIST": "0"}, {"KSCHED_PERSIST": "0", "KSCHED_DEVICE_HANDOFF": "1"},
+                                 {"KSCHED_PERSIST": "0", "KSCHED_SCORE_EVENT": "1"}],
+                         ids=["stream", "stream_merge_poll", "stream_score_event"])
 def test_pipeline_variants_parity(gpu_available, oracle_mod, env, monkeypatch):
-    """The alternative hand-offs of the batched pipeline stay bit-exact: the merge
-    polling Ctl::scored instead of a stream event, and the score waiting on a stream event instead of
-    polling Ctl::committed.  Each is selected by its environment switch at enqueue time."""
+    """Single-rank batched mode runs the persistent pipeline by default (ksched_persist.hip); the stream
+    pipeline (per-batch launches; the multi-rank path) and its alternative hand-offs -- the merge polling
+    Ctl::scored instead of a stream event, the score waiting on a stream event instead of polling
+    Ctl::committed -- stay bit-exact.  Selected by environment switches at enqueue time."""
     from ksched import MODE_BATCHED, cluster
-    monkeypatch.setenv(env, "1")
-    for name, nn, pp in (("c3", 30000, 2000), ("c5", 40000, 1500)):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for name, nn, pp in (("c3", 30000, 2000), ("c5", 40000, 1500), ("c5hc", 20000, 3000)):
         cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
         want = oracle_mod.schedule(cl, nthreads=8)
-        assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=64), want, f"{name}/{env}")
+        for kw in (dict(topk=16, batch=64), dict(topk=8, batch=32, chunk_topk=2)):
+            got = run_engine(cl, MODE_BATCHED, **kw)
+            assert_same(got, want, f"{name}/{env}/{kw}")
+            assert got[4]["pipeline"] == "stream", got[4]
 
 
-def test_signed_zero_prices_keep_lowest_index(gpu_available, oracle_mod):
-    """Prices 0 and -0 are the same price: the lowest node index must win in every mode, including
-    when the two nodes land in different score workgroups and are ranked by key bits in the merge."""
-    from ksched import cluster
-    n, p = 6000, 400
-    rng = np.random.default_rng(7)
-    price = (1.0 + rng.integers(0, 50, size=n) / 8).astype(np.float32)
-    zeros = [3, 700, 1500, 2999, 4100, 5998]
-    for k, j in enumerate(zeros):
-        price[j] = np.float32(-0.0) if k % 2 else np.float32(0.0)
-    cl = cluster.Cluster(name="signed-zero", alloc_cpu=np.full(n, 4000, np.int64),
-                         alloc_mem=np.full(n, 8 << 20, np.int64), alloc_pods=np.full(n, 110, np.int64),
-                         req_cpu=rng.integers(100, 1500, size=p).astype(np.int64),
-                         req_mem=rng.integers(1, 1 << 20, size=p).astype(np.int64), req_pods=np.ones(p, np.int64),
-                         price=price, priority=cluster.PRIORITY_BEST_PRICE, domain=cluster.DOMAIN_FEASIBLE)
-    want = oracle_mod.schedule(cl)
-    assert want[0][0] == 3 and not np.signbit(want[1][0])
-    for name, mode, kw in modes():
-        assert_same(run_engine(cl, mode, **kw), want, f"signed-zero/{name}")
-
-
-def test_load_nodes_rejects_index_overflow(gpu_available):
-    """Global node indices are int32 with INT32_MAX reserved for "no candidate"."""
-    from ksched import Engine, KschedError
-    one = np.ones(4, np.int64)
-    with Engine(node_offset=(1 << 31) - 18, nodes_global=1 << 31) as e:
-        with pytest.raises(KschedError):
-            e.load_nodes(one, one, one)
+@pytest.mark.parametrize("name,nn,pp", [("c3", 30000, 2000), ("c5", 40000, 1500), ("c5hc", 20000, 3000),
+                                         ("c2", 5000, 2000), ("c1", 700, 300)])
+def test_persistent_pipeline_parity(gpu_available, oracle_mod, name, nn, pp):
+    """The default single-rank batched path is the persistent pipeline (ksched_persist.hip: a resident
+    score grid of up to CUs - 8 workgroups + one resident commit workgroup); the stats say it ran, and it
+    is bit-exact at every (topk, batch, chunk_topk) it accepts -- including the grid sizes where the
+    score workgroups outnumber the batch (non-merger workgroups run a batch ahead)."""
+    from ksched import MODE_BATCHED, cluster
+    cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    for kw in (dict(topk=16, batch=64), dict(topk=8, batch=64, chunk_topk=8), dict(topk=4, batch=32, chunk_topk=2),
+               dict(topk=16, batch=16)):
+        got = run_engine(cl, MODE_BATCHED, **kw)
+        assert_same(got, want, f"{name}/{kw}")
+        assert got[4]["pipeline"] == "persistent", got[4]
