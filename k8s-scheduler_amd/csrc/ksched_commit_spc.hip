@@ -88,6 +88,16 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int src) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// plan_after_commit for the persistent commit: the plans come from (and go to) its LDS copy too
+__device__ __forceinline__ void persist_plan(const CommitArgs &A, bool truncated, int64_t cursor) {
+    PersistLocal *L = A.loc;
+    const int64_t n1 = L->plan[(A.batch + 1) % kPlanRing];
+    int64_t nx = truncated ? cursor : (n1 < 0 ? -1 : n1 + A.B);
+    if (nx >= A.pods.p) nx = -1;
+    L->plan[(A.batch + 2) % kPlanRing] = nx;
+    st_coh(A.plan2, (uint64_t)nx);
+}
+
 __device__ __forceinline__ void lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -111,20 +121,46 @@ __device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64
 // One batch's ordered commit by the whole workgroup (kSpcThreads).  COH: the lists arrive from other
 // workgroups of a running persistent kernel (sc1 loads), and what the score workgroups read back --
 // the XBuf export, the next plans, the cursor -- leaves as sc1 stores (ksched_persist.hip).
+// a batch's pod requests, lane = pod (loaded early by the persistent commit, before its wait)
+struct LanePods {
+    int64_t rc, rm, rp;
+    uint64_t sel;
+};
+
+template <bool LAB>
+__device__ __forceinline__ LanePods load_lane_pods(const PodArgs &pods, int64_t p0, int nb) {
+    const int lane = threadIdx.x & 63;
+    const bool pj = lane < nb;
+    LanePods q;
+    q.rc = pj ? pods.rc[p0 + lane] : 0;
+    q.rm = pj ? pods.rm[p0 + lane] : 0;
+    q.rp = pj ? pods.rp[p0 + lane] : 0;
+    q.sel = (LAB && pj) ? pods.sel[p0 + lane] : 0;
+    return q;
+}
+
 template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH>
-__device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem) {
+__device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int64_t p0 = load_i64<COH>(A.plan);
-    const int64_t cursor = load_i64<COH>(&A.ctl->cursor);
+    PersistLocal *const L = A.loc;
+    const int64_t p0 = COH ? L->plan[A.batch % kPlanRing] : load_i64<COH>(A.plan);
+    const int64_t cursor = COH ? L->cursor : load_i64<COH>(&A.ctl->cursor);
     if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
         // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
         if (wave == 0) {
             if (lane == 0) {
-                if (COH) st_coh(&A.xout->count, 0ull); else A.xout->count = 0;
-                if (p0 >= 0 && p0 < A.pods.p) add_i64<COH>(&A.ctl->stats[3], 1);
-                plan_after_commit<COH>(A, false, cursor);
+                if (COH) {
+                    st_coh(&A.xout->count, 0ull);
+                    L->xcount = 0;
+                    if (p0 >= 0 && p0 < A.pods.p) st_coh(&A.ctl->stats[3], (uint64_t)++L->stats[3]);
+                    persist_plan(A, false, cursor);
+                } else {
+                    A.xout->count = 0;
+                    if (p0 >= 0 && p0 < A.pods.p) add_i64<COH>(&A.ctl->stats[3], 1);
+                    plan_after_commit<COH>(A, false, cursor);
+                }
             }
             publish_committed<COH>(A);
         }
@@ -160,10 +196,9 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
     // Issued before the prologue so these global loads overlap the list loads instead of following
     // them behind a barrier.
     const bool pj = lane < nb;
-    const int64_t rc = pj ? A.pods.rc[p0 + lane] : 0;
-    const int64_t rm = pj ? A.pods.rm[p0 + lane] : 0;
-    const int64_t rp = pj ? A.pods.rp[p0 + lane] : 0;
-    const uint64_t sel = (LAB && pj) ? A.pods.sel[p0 + lane] : 0;
+    const LanePods lp = pre ? *pre : load_lane_pods<LAB>(A.pods, p0, nb);
+    const int64_t rc = lp.rc, rm = lp.rm, rp = lp.rp;
+    const uint64_t sel = lp.sel;
     const int64_t fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
     const int cut0 = (wave == 0 && pj) ? load_rec<COH>(A.lists + (size_t)lane * K).pad : 0;
 
@@ -183,9 +218,9 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
         m.LI[q * 64 + j] = idx;
         m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
     }
-    const int nin = COH ? (int)(uint32_t)ld_coh(&A.xin->count) : A.xin->count;  // <= 64
+    const int nin = COH ? L->xcount : A.xin->count;  // <= 64
     for (int e = tid; e < nin; e += kSpcThreads) {
-        const XRec xi = load_xrec<COH>(&A.xin->e[e]);
+        const XRec xi = COH ? L->xe[e] : A.xin->e[e];
         SpcSlot &x = m.T[e];
         x.idx = xi.idx; x.mine = 0;
         for (int r = 0; r < 3; ++r) { x.s0[r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
@@ -550,17 +585,31 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
             o.sb[0] = x.sb[0]; o.sb[1] = x.sb[1]; o.sb[2] = x.sb[2];
             o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
             o.labels = x.labels; o.price = x.price; o.pad2 = 0;
-            store_xrec<COH>(&A.xout->e[base + __popcll(mask & ((1ull << lane) - 1))], o);
+            const int slot = base + __popcll(mask & ((1ull << lane) - 1));
+            store_xrec<COH>(&A.xout->e[slot], o);
+            if (COH) L->xe[slot] = o;  // the next batch inherits it from LDS (every inherited read is done)
         }
         base += __popcll(mask);
     }
     if (lane == 0) {
-        if (COH) st_coh(&A.xout->count, (uint64_t)(uint32_t)base); else A.xout->count = base;
-        store_i64<COH>(&A.ctl->cursor, p0 + done);
-        add_i64<COH>(&A.ctl->stats[0], 1);
-        add_i64<COH>(&A.ctl->stats[1], (done < nb) ? 1 : 0);
-        add_i64<COH>(&A.ctl->stats[2], placed);
-        plan_after_commit<COH>(A, done < nb, p0 + done);
+        if (COH) {
+            st_coh(&A.xout->count, (uint64_t)(uint32_t)base);
+            L->xcount = base;
+            L->cursor = p0 + done;
+            st_coh(&A.ctl->cursor, (uint64_t)(p0 + done));
+            L->stats[0] += 1;
+            L->stats[1] += (done < nb) ? 1 : 0;
+            L->stats[2] += placed;
+            for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
+            persist_plan(A, done < nb, p0 + done);
+        } else {
+            A.xout->count = base;
+            store_i64<COH>(&A.ctl->cursor, p0 + done);
+            add_i64<COH>(&A.ctl->stats[0], 1);
+            add_i64<COH>(&A.ctl->stats[1], (done < nb) ? 1 : 0);
+            add_i64<COH>(&A.ctl->stats[2], placed);
+            plan_after_commit<COH>(A, done < nb, p0 + done);
+        }
         if (A.dbg) {
             A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1;
             A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
@@ -593,11 +642,20 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
     __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     __shared__ int s_stop;
+    __shared__ PersistLocal loc;
     Ctl *ctl = P.ctl;
+    // k_ctl_init ran before this kernel on the stream: take the initial plans / cursor / stats once
+    if (threadIdx.x < kPlanRing) loc.plan[threadIdx.x] = (int64_t)ld_coh(&ctl->plan[threadIdx.x]);
+    if (threadIdx.x == 0) {
+        loc.cursor = (int64_t)ld_coh(&ctl->cursor);
+        for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_coh(&ctl->stats[i]);
+        loc.xcount = 0;
+    }
+    __syncthreads();
     int64_t nact = 0;
     int idle = 0;
     for (int64_t b = 0;; ++b) {
-        const int64_t p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);  // written by this workgroup / k_ctl_init
+        const int64_t p0 = loc.plan[b % kPlanRing];  // written by this workgroup (or k_ctl_init)
         if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
             // pods remain but nothing is planned: a truncation re-plans within two batches, so this is a
             // protocol error -- stop everyone instead of spinning
@@ -607,9 +665,12 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
             }
             return;
         }
+        LanePods pre{0, 0, 0, 0};
         if (p0 >= 0 && p0 < P.pods.p) {
             idle = 0;
             ++nact;
+            // the pods' requests are known now: their loads overlap the wait for the merges
+            if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
             if (threadIdx.x == 0) {
                 const uint64_t t0 = wall_clock64();
                 s_stop = 0;
@@ -643,10 +704,12 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         ca.out = P.out;
         ca.batch = b;
         ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
-        commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem);
+        ca.dbg = P.cdbg;
+        ca.loc = &loc;
+        commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem, &pre);
         __syncthreads();
         if (threadIdx.x == 0) trace_at(P, b, 4);
-        if ((int64_t)ld_coh(&ctl->cursor) >= P.pods.p) {
+        if (loc.cursor >= P.pods.p) {
             if (threadIdx.x == 0)
                 __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;

@@ -89,7 +89,8 @@ struct ksched_ctx {
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
     int64_t *d_mdbg = nullptr;    // KSCHED_MERGE_STAMPS diagnostics
     hipStream_t stream2 = nullptr;  // merge + commit stream of the batched pipeline
-    hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[2] = {};
+    hipStream_t stream3 = nullptr;  // persistent pipeline: the merger workgroups' stream (created on first use)
+    hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[3] = {};
     void *d_xring = nullptr, *d_lring = nullptr;
     int64_t xring_bytes = 0, lring_bytes = 0;
     // exact workspace
@@ -480,7 +481,7 @@ void print_persist_trace(ksched_ctx *c) {
     std::vector<uint64_t> t((size_t)c->trace_cap * kTraceCols);
     if (hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
-    double sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double sum[14] = {};
     int64_t cnt = 0, first = -1, last = -1;
     for (int64_t b = 2; b < c->trace_cap; ++b) {
         if (!at(b, 0) || !at(b, 1) || !at(b, 2) || !at(b, 3) || !at(b, 4) || !at(b - 2, 4)) continue;
@@ -497,15 +498,37 @@ void print_persist_trace(ksched_ctx *c) {
         sum[7] += (double)(int64_t)(at(b, 0) - at(b, 6));      // WG 0: plan loads + XBuf apply
         sum[8] += (double)(int64_t)(at(b, 5) - at(b, 0));      // WG 0: score + fold + list stores
         sum[9] += (double)(int64_t)(at(b, 7) - at(b, 1));      // last arrival -> merger past its poll
+        sum[10] += (double)(int64_t)(at(b, 8) - at(b, 0));     // WG 0 wave 0: row loop (incl. pod loads)
+        sum[11] += (double)(int64_t)(at(b, 9) - at(b, 8));     // WG 0: waiting for its slowest wave
+        sum[12] += (double)(int64_t)(at(b, 10) - at(b, 9));    // WG 0: fold
+        sum[13] += (double)(int64_t)(at(b, 5) - at(b, 10));    // WG 0: list stores + drain
+    }
+    if (c->d_dbg) {
+        int64_t hd[16];
+        if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14])
+            fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f failures %lld | cycles/batch: prologue %.0f "
+                    "guess %.0f evaluate %.0f check %.0f total %.0f\n", (long long)hd[14], (double)hd[12] / hd[14],
+                    (long long)hd[13], (double)hd[0] / hd[14], (double)hd[1] / hd[14], (double)hd[2] / hd[14],
+                    (double)hd[3] / hd[14], (double)hd[4] / hd[14]);
+    }
+    if (c->d_mdbg) {
+        int64_t hm[8];
+        if (hipMemcpy(hm, c->d_mdbg, sizeof(hm), hipMemcpyDeviceToHost) == hipSuccess && hm[7]) {
+            const double nwg = (double)hm[7];
+            fprintf(stderr, "persist merge: merges=%lld | cycles/merge: loads %.0f rank-heads %.0f barrier %.0f "
+                    "global-heads %.0f rank-entries %.0f write %.0f\n", (long long)hm[7], hm[0] / nwg, hm[1] / nwg,
+                    hm[2] / nwg, hm[3] / nwg, hm[4] / nwg, hm[5] / nwg);
+        }
     }
     if (!cnt) return;
     const double us = 0.01 / (double)cnt;  // 100 MHz ticks -> us, mean
     fprintf(stderr,
             "persist trace: %lld batches, period %.2f us | to-score %.2f score %.2f merge %.2f to-commit %.2f "
-            "commit %.2f commit-gap %.2f | wg0: poll %.2f apply %.2f score %.2f | merger poll %.2f\n",
+            "commit %.2f commit-gap %.2f | wg0: poll %.2f apply %.2f score %.2f (rows %.2f slowest-wave %.2f fold %.2f "
+            "stores %.2f) | merger poll %.2f\n",
             (long long)cnt, 0.01 * (double)(int64_t)(at(last, 4) - at(first, 4)) / (double)std::max<int64_t>(1, last - first),
             sum[0] * us, sum[1] * us, sum[2] * us, sum[3] * us, sum[4] * us, sum[5] * us, sum[6] * us, sum[7] * us,
-            sum[8] * us, sum[9] * us);
+            sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
 }
 
 constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
@@ -520,8 +543,8 @@ int enqueue_persistent(ksched_ctx *c) {
     // free on EVERY XCD for the commit workgroup to be guaranteed a place: G <= CUs - 8 (measured: with
     // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts)
     const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - kXcds));
-    const int G = (int)std::max<int64_t>(B, std::min<int64_t>(gcap, (n + 15) / 16));
-    if (G < B || G > c->cus - kXcds) return 1;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n + 15) / 16));
+    if (G > c->cus - kXcds) return 1;
     const int R = (int)((n + G - 1) / G);
     const size_t lds = persist_score_lds(KC, R);
     if (lds == 0) return 1;
@@ -566,16 +589,31 @@ int enqueue_persistent(ksched_ctx *c) {
         a.trace = c->d_trace;
         a.trace_cap = c->trace_cap;
     }
-    hipStream_t sS = c->stream, sC = c->stream2;
+    if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
+    if (c->d_dbg) {
+        HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), c->stream));
+        a.cdbg = c->d_dbg;
+    }
+    if (env_int("KSCHED_MERGE_STAMPS", 0) && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
+    if (c->d_mdbg) {
+        HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), c->stream));
+        a.mdbg = c->d_mdbg;
+    }
+    if (!c->stream3) HIPCHK(c, hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
+    hipStream_t sS = c->stream, sC = c->stream2, sM = c->stream3;
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
-    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit stream starts after the initialisation
+    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit and merge streams start after the initialisation
     HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
-    const hipError_t e = launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC);
+    HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
+    const hipError_t e =
+        launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC, sM);
     if (e == hipErrorInvalidValue) return 1;  // does not fit after all: the stream pipeline runs
     if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("launch_persist: ") + hipGetErrorString(e));
-    HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));  // the run's end event on stream S covers the commit
+    HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));  // the run's end event on stream S covers commit + merge
     HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
+    HIPCHK(c, hipEventRecord(c->ev_pipe[2], sM));
+    HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[2], 0));
     HIPCHK(c, hipMemcpyAsync(c->h_cursor, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, sS));
     c->persist_stats = true;
     c->persist_B = B;
@@ -675,7 +713,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
         ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_lists[i], hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&c->ev_commit[i], hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&c->ev_scored[i], hipEventDisableTiming) == hipSuccess;
-    for (int i = 0; i < 2; ++i) ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming) == hipSuccess;
+    for (int i = 0; i < 3; ++i) ev_ok = ev_ok && hipEventCreateWithFlags(&c->ev_pipe[i], hipEventDisableTiming) == hipSuccess;
     if (!ev_ok || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
@@ -698,6 +736,7 @@ int ksched_destroy(ksched_ctx *c) {
     hipSetDevice(c->dev);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->stream2) hipStreamSynchronize(c->stream2);
+    if (c->stream3) hipStreamSynchronize(c->stream3);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
@@ -712,11 +751,12 @@ int ksched_destroy(ksched_ctx *c) {
         if (c->ev_commit[i]) hipEventDestroy(c->ev_commit[i]);
         if (c->ev_scored[i]) hipEventDestroy(c->ev_scored[i]);
     }
-    for (int i = 0; i < 2; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
+    for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
     hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
+    if (c->stream3) hipStreamDestroy(c->stream3);
     delete c;
     return KSCHED_OK;
 }

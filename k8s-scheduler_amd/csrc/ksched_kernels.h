@@ -165,9 +165,24 @@ struct MergeArgs {
     const int64_t *cursor;
     int64_t P;
     int32_t B;
+    int32_t p0_known;   // 1: p0v is this batch's first pod (the persistent score grid read it already)
+    int64_t p0v;
     const unsigned long long *wait_ctr;  // k_merge_pod: poll until *wait_ctr >= wait_target (null: no wait)
     unsigned long long wait_target;
     int32_t *err;                        // device error word (2 = the wait timed out)
+};
+
+// The persistent commit workgroup's private control state (LDS): it is the only writer of the plans,
+// the cursor, the stats and the export once its kernel runs, so it reads its own copies instead of
+// loading them back from HBM -- every global load of the commit's serial chain costs ~1-2 us.
+struct PersistLocal {
+    int64_t plan[kPlanRing];
+    int64_t cursor;
+    int64_t stats[5];
+    int32_t xcount;   // the previous batch's export (this batch's inherited nodes)
+    int32_t pad;
+    XRec xe[64];
+    // the batch's pods, loaded before the wait for the merges (lane = pod)
 };
 
 struct CommitArgs {
@@ -185,6 +200,7 @@ struct CommitArgs {
     int64_t *dbg;           // diagnostics only (KSCHED_COMMIT_STAMPS): per-phase cycle sums, else null
     int64_t batch;          // this batch's index in the call (published to Ctl::committed when done)
     int64_t *cursor_at;     // persistent pipeline: &Ctl::cursor_at[batch % kPlanRing] (else null)
+    PersistLocal *loc;      // persistent pipeline (COH): the commit workgroup's LDS control state
 };
 
 // Commit(b) -> score(b+2) hand-off on the device: the committing wave drains its stores, writes back the
@@ -194,7 +210,8 @@ struct CommitArgs {
 // COH (persistent pipeline): every handed-off store was an sc1 store, so no L2 write-back is needed.
 template <bool COH = false>
 __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
-    if ((threadIdx.x & 63) == 0 && A.cursor_at) st_coh(A.cursor_at, ld_coh(&A.ctl->cursor));
+    if ((threadIdx.x & 63) == 0 && A.cursor_at)
+        st_coh(A.cursor_at, COH ? (uint64_t)A.loc->cursor : ld_coh(&A.ctl->cursor));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((threadIdx.x & 63) == 0) {
         if (!COH) {
@@ -319,9 +336,11 @@ struct PersistArgs {
     // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
     uint64_t *trace;
     int64_t trace_cap;
+    int64_t *cdbg;  // KSCHED_COMMIT_STAMPS: commit phase cycle sums (CommitArgs::dbg), else null
+    int64_t *mdbg;  // KSCHED_MERGE_STAMPS: merge phase cycle sums (MergeArgs::dbg), else null
 };
 // trace columns: score start (WG 0 past its wait), last arrival, last merge done, commit start, commit end
-constexpr int kTraceCols = 8;
+constexpr int kTraceCols = 16;
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }
@@ -329,7 +348,7 @@ hipError_t launch_persist_commit(int K, int prio, int dom, bool lab, bool fast53
 // bytes of dynamic LDS the score grid needs (0: the rows do not fit -> use the stream pipeline)
 size_t persist_score_lds(int KC, int rows_per_wg);
 hipError_t launch_persist(int KC, int K, int prio, int dom, bool lab, bool fast53, const PersistArgs &a, size_t lds,
-                          hipStream_t score_stream, hipStream_t commit_stream);
+                          hipStream_t score_stream, hipStream_t commit_stream, hipStream_t merge_stream);
 hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s);
 // diagnostics: qdiv(a, b, recip(b)) against the native a / b, bit for bit
 hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,

@@ -77,7 +77,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
     const bool dbg = A.dbg != nullptr;
     uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
-    const int64_t p0 = load_i64<COH>(A.cursor);
+    const int64_t p0 = A.p0_known ? A.p0v : load_i64<COH>(A.cursor);
     if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // workgroup-uniform
     if (A.wait_ctr) wait_scored(A.wait_ctr, A.wait_target, A.err);
     const bool has = tid < A.C_in;
@@ -121,8 +121,9 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         if (lane == 0) { s_wck[wave] = bc; s_wci[wave] = bi; s_wcut[wave] = wcut; s_wcnt[wave] = wc; s_wnv[wave] = nv; }
     }
     __syncthreads();
-    // 1. rank each head within its wave (broadcast reads, independent compares)
-    {
+    // 1. rank each head within its wave (broadcast reads, independent compares; waves without lists idle)
+    const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
+    if (wave < nw) {
         int rank = 0;
         const int base = wave * 64;
 #pragma unroll 16
@@ -138,7 +139,6 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
     __syncthreads();
     if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
     // 2. rank the survivors against each other
-    const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
     int ntot = 0;  // valid heads in total (survivors: the first min(K, nv) slots of each wave)
     for (int w = 0; w < nw; ++w) ntot += s_wnv[w];
     if (tid < nw * K) {
@@ -149,7 +149,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
             const int32_t mi = s_cidx[tid];
             int g = 0;
 #pragma unroll 16
-            for (int c = 0; c < W * K; ++c) g += code_better(s_ccode[c], s_cidx[c], mc, mi) ? 1 : 0;
+            for (int c = 0; c < nw * K; ++c) g += code_better(s_ccode[c], s_cidx[c], mc, mi) ? 1 : 0;
             if (g < K) s_keep[g] = s_clist[tid];
         }
     }

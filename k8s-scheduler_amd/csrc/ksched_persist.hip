@@ -29,7 +29,11 @@ namespace ksched {
 namespace {
 
 constexpr int kPW = 8;                     // score waves per workgroup
-constexpr int kPThreads = kPW * 64;        // == kMergeThreads: a merger runs merge_pod_body as is
+constexpr int kPThreads = kPW * 64;
+#ifndef KSCHED_PERSIST_PU
+#define KSCHED_PERSIST_PU 4
+#endif
+constexpr int kPU = KSCHED_PERSIST_PU;     // rows per score step (independent key chains)        // == kMergeThreads: a merger runs merge_pod_body as is
 constexpr size_t kExclusiveLds = 81 * 1024;  // > 160 KiB / 2: one score workgroup per CU
 
 __device__ __forceinline__ bool spin_ge(const unsigned long long *p, unsigned long long v, int64_t limit) {
@@ -62,7 +66,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
     int32_t *s_idx = reinterpret_cast<int32_t *>(fold + (size_t)(kPW / 2) * KC * 64 * 8);
     int32_t *s_cnt = s_idx + (size_t)(kPW / 2) * KC * 64;                 // [64]
     __shared__ int64_t s_p0, s_done;
-    __shared__ int s_stop, s_rank;
+    __shared__ int s_stop;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -141,30 +145,46 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
 #pragma unroll
         for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
         int32_t cnt = 0;
-        for (int r = wave; r < R; r += kPW) {
-            const int64_t j = g + (int64_t)r * G;
-            if (j >= n) break;
-            const NodeRec &nd = rows[r];
-            const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
-            const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
-            cnt += f;
-            double k;
-            const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1],
-                                                          nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k);
-            double ck = el ? k : -__builtin_inf();
-            int32_t ci = (int32_t)j;
-            bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
+        // kPU rows per step: their keys are independent f64 chains the scheduler interleaves (two waves
+        // per SIMD hide little latency on their own); inserted in ascending node order afterwards
+        for (int r0 = wave; r0 < R; r0 += kPW * kPU) {
+            double ks[kPU];
 #pragma unroll
-            for (int q = 0; q < KC; ++q) {
-                const bool sw = moved || ck > key[q];
-                moved = sw;
-                const double tk = key[q];
-                const int32_t ti = idx[q];
-                key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
-                ck = sw ? tk : ck; ci = sw ? ti : ci;
+            for (int u = 0; u < kPU; ++u) {
+                const int r = r0 + u * kPW;
+                const int64_t j = g + (int64_t)r * G;
+                ks[u] = -__builtin_inf();
+                if (r < R && j < n) {  // wave-uniform
+                    const NodeRec &nd = rows[r];
+                    const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+                    const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
+                    cnt += f;
+                    double k;
+                    const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0],
+                                                                  nd.af[1], nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3,
+                                                                  nd.price, &k);
+                    ks[u] = el ? k : -__builtin_inf();
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kPU; ++u) {
+                double ck = ks[u];
+                int32_t ci = (int32_t)(g + (int64_t)(r0 + u * kPW) * G);
+                bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    const bool sw = moved || ck > key[q];
+                    moved = sw;
+                    const double tk = key[q];
+                    const int32_t ti = idx[q];
+                    key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+                    ck = sw ? tk : ck; ci = sw ? ti : ci;
+                }
             }
         }
+        if (g == 0 && tid == 0) trace_at(P, b, 8);
         __syncthreads();  // s_cnt zeroed before any wave adds
+        if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
         // fold the wave lists pairwise: W -> W/2 -> ... -> 1 (a list that is cut when full folds into
         // the top-KC of the union, again cut when full: DESIGN.md section 4)
@@ -188,6 +208,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
             }
             __syncthreads();
         }
+        if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
         Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
         int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
@@ -202,41 +223,14 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
         }
         drain_stores();
         __syncthreads();
-        // ---- arrive; the last B arrivals of the batch merge one pod each ----
+        // ---- arrive (the merger workgroups, k_persist_merge, wait for all G) ----
         const int slot = (int)((nact - 1) % 4);
-        const unsigned long long use = (unsigned long long)((nact - 1) / 4);  // earlier uses of the slot
         if (tid == 0) {
             if (g == 0) trace_at(P, b, 5);
             const unsigned long long old = __hip_atomic_fetch_add(&ctl->arrive[slot], 1ull, __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
-            s_rank = (int)(old - use * (unsigned long long)G);
-        }
-        __syncthreads();
-        const int rank = s_rank;
-        if (rank == G - 1 && tid == 0) trace_at(P, b, 1);
-        if (rank >= G - P.B) {
-            if (tid == 0) {
-                s_stop = spin_ge(&ctl->arrive[slot], (use + 1) * (unsigned long long)G, P.timeout_ticks) ? 0 : 1;
-                if (s_stop) set_err(P.err, 7);
-            }
-            __syncthreads();
-            if (s_stop) return;
-            if (rank == G - 1 && tid == 0) trace_at(P, b, 7);
-            char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
-            MergeArgs ma{};
-            ma.in = part; ma.in_cnt = part_cnt; ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
-            ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
-            ma.nodes = P.nodes; ma.node_offset = 0;
-            ma.out_rec = reinterpret_cast<Rec *>(lb);
-            ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
-            merge_pod_body<KC, K, true>(ma, rank - (G - P.B));
-            drain_stores();
-            __syncthreads();
-            if (tid == 0) {
-                const unsigned long long m =
-                    __hip_atomic_fetch_add(&ctl->merged[slot], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (m + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
-            }
+            const unsigned long long use = (unsigned long long)((nact - 1) / 4);
+            if (old + 1 == (use + 1) * (unsigned long long)G) trace_at(P, b, 1);
         }
     }
     // every pod is resolved: this workgroup's rows go back to HBM whole (allocatable, cached doubles,
@@ -248,8 +242,80 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
     }
 }
 
+// The merge side: B workgroups, one per pod slot of a batch, resident beside the score grid (small LDS).
+// Per active batch: wait for the G arrivals, merge pod m's G lists into its K-entry Rec list (sc1),
+// count the merge.  The score workgroups never merge, so a merge never delays the next batch's scan.
+template <int KC, int K>
+__global__ __launch_bounds__(kMergeThreads) void k_persist_merge(PersistArgs P) {
+    __shared__ int64_t s_p0, s_done;
+    __shared__ int s_stop;
+    const int tid = threadIdx.x;
+    const int m = blockIdx.x;
+    const int G = P.G;
+    const int64_t NP = P.pods.p;
+    Ctl *ctl = P.ctl;
+    int64_t nact = 0;
+    int idle = 0;
+    for (int64_t b = 0;; ++b) {
+        if (tid == 0) {
+            int stop = 0;
+            if (b >= 2 && !spin_ge(&ctl->committed, (unsigned long long)(b - 1), P.timeout_ticks)) {
+                set_err(P.err, 6);
+                stop = 2;
+            }
+            s_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+            s_done = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+            if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
+            s_stop = stop;
+        }
+        __syncthreads();
+        if (s_stop) return;
+        const int64_t p0 = s_p0;
+        if (s_done >= NP) return;
+        if (p0 < 0 || p0 >= NP) {
+            if (++idle > kPlanRing) {
+                if (tid == 0) set_err(P.err, 8);
+                return;
+            }
+            __syncthreads();  // s_p0 / s_done are rewritten next iteration
+            continue;
+        }
+        idle = 0;
+        ++nact;
+        const int slot = (int)((nact - 1) % 4);
+        const unsigned long long use = (unsigned long long)((nact - 1) / 4);
+        if (tid == 0) {
+            s_stop = spin_ge(&ctl->arrive[slot], (use + 1) * (unsigned long long)G, P.timeout_ticks) ? 0 : 1;
+            if (s_stop) set_err(P.err, 7);
+            if (m == 0) trace_at(P, b, 7);
+        }
+        __syncthreads();
+        if (s_stop) return;
+        const size_t part_elems = (size_t)P.B * G;
+        char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
+        MergeArgs ma{};
+        ma.in = P.part + (size_t)(b % 2) * part_elems * KC;
+        ma.in_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
+        ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
+        ma.p0_known = 1; ma.p0v = p0;
+        ma.nodes = P.nodes; ma.node_offset = 0;
+        ma.dbg = P.mdbg;
+        ma.out_rec = reinterpret_cast<Rec *>(lb);
+        ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
+        merge_pod_body<KC, K, true>(ma, m);
+        drain_stores();
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long d =
+                __hip_atomic_fetch_add(&ctl->merged[slot], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (d + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
+        }
+    }
+}
+
 size_t persist_score_lds(int KC, int rows_per_wg) {
-    // merge_pod_body's static arrays come on top: 512 lists x KC x 12 B + ~4 KiB
+    // a merger workgroup (merge_pod_body's static arrays: 512 lists x KC x 12 B + ~4 KiB) must fit beside
     const size_t need = (size_t)rows_per_wg * sizeof(NodeRec) + (size_t)(kPW / 2) * KC * 64 * 12 + 64 * 4;
     const size_t static_merge = (size_t)kMergeThreads * KC * 12 + 4096;
     if (need + static_merge > 160 * 1024) return 0;
@@ -259,50 +325,69 @@ size_t persist_score_lds(int KC, int rows_per_wg) {
 namespace {
 
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
-hipError_t persist_one(const PersistArgs &a, size_t lds, hipStream_t s) {
+hipError_t persist_one(const PersistArgs &a, size_t lds, hipStream_t s, hipStream_t sm, bool launch) {
     auto fn = k_persist_score<KC, K, PRIO, DOM, LAB, F53>;
-    hipFuncAttributes at{};
+    auto fm = k_persist_merge<KC, K>;
+    hipFuncAttributes at{}, am{};
     hipError_t e = hipFuncGetAttributes(&at, (const void *)fn);
     if (e != hipSuccess) return e;
-    if (at.sharedSizeBytes + lds > 160 * 1024) return hipErrorInvalidValue;  // caller falls back
+    e = hipFuncGetAttributes(&am, (const void *)fm);
+    if (e != hipSuccess) return e;
+    // one score workgroup + one merger workgroup per CU: LDS, and two waves per SIMD of each in the
+    // 512-entry VGPR file (granule 8) -- otherwise the caller falls back to the stream pipeline
+    auto vg = [](int r) { return (r + 7) / 8 * 8; };
+    if (at.sharedSizeBytes + lds + am.sharedSizeBytes > 160 * 1024) return hipErrorInvalidValue;
+    if (2 * vg(at.numRegs) + 2 * vg(am.numRegs) > 512) return hipErrorInvalidValue;
+    if (!launch) return hipSuccess;
     e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    // a plain launch: G <= CUs - 1 workgroups that each exclude a second one from their CU are all
-    // resident beside the commit workgroup (a cooperative launch would wait for the running commit
-    // kernel to drain first -- measured: it never starts)
+    // plain launches: G <= CUs - 8 score workgroups that each exclude a second one from their CU are
+    // all resident beside the commit workgroup; the B mergers fit beside them (a cooperative launch
+    // would wait for the running commit kernel to drain first -- measured: it never starts)
     hipLaunchKernelGGL(fn, dim3(a.G), dim3(kPThreads), lds, s, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fm, dim3(a.B), dim3(kMergeThreads), 0, sm, a);
     return hipGetLastError();
 }
 
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
-hipError_t persist_k(int K, const PersistArgs &a, size_t lds, hipStream_t s) {
+hipError_t persist_k(int K, const PersistArgs &a, size_t lds, hipStream_t s, hipStream_t sm, bool launch) {
     switch (K) {
-        case 4: return KC <= 4 ? persist_one<(KC <= 4 ? KC : 4), 4, PRIO, DOM, LAB, F53>(a, lds, s) : hipErrorInvalidValue;
-        case 8: return KC <= 8 ? persist_one<(KC <= 8 ? KC : 8), 8, PRIO, DOM, LAB, F53>(a, lds, s) : hipErrorInvalidValue;
-        case 16: return persist_one<KC, 16, PRIO, DOM, LAB, F53>(a, lds, s);
+        case 4: return KC <= 4 ? persist_one<(KC <= 4 ? KC : 4), 4, PRIO, DOM, LAB, F53>(a, lds, s, sm, launch) : hipErrorInvalidValue;
+        case 8: return KC <= 8 ? persist_one<(KC <= 8 ? KC : 8), 8, PRIO, DOM, LAB, F53>(a, lds, s, sm, launch) : hipErrorInvalidValue;
+        case 16: return persist_one<KC, 16, PRIO, DOM, LAB, F53>(a, lds, s, sm, launch);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <int PRIO, int DOM, bool LAB, bool F53>
-hipError_t persist_kc(int KC, int K, const PersistArgs &a, size_t lds, hipStream_t s) {
+hipError_t persist_kc(int KC, int K, const PersistArgs &a, size_t lds, hipStream_t s, hipStream_t sm, bool launch) {
     switch (KC) {
-        case 2: return persist_k<2, PRIO, DOM, LAB, F53>(K, a, lds, s);
-        case 4: return persist_k<4, PRIO, DOM, LAB, F53>(K, a, lds, s);
-        case 8: return persist_k<8, PRIO, DOM, LAB, F53>(K, a, lds, s);
+        case 2: return persist_k<2, PRIO, DOM, LAB, F53>(K, a, lds, s, sm, launch);
+        case 4: return persist_k<4, PRIO, DOM, LAB, F53>(K, a, lds, s, sm, launch);
+        case 8: return persist_k<8, PRIO, DOM, LAB, F53>(K, a, lds, s, sm, launch);
         default: return hipErrorInvalidValue;
     }
+}
+
+hipError_t persist_grid(int KC, int K, int prio, int dom, bool lab, bool f53, const PersistArgs &a, size_t lds,
+                        hipStream_t s, hipStream_t sm, bool launch) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (persist_kc<P_, D_, L_, F_>(KC, K, a, lds, s, sm, launch)));
 }
 
 }  // namespace
 
 hipError_t launch_persist(int KC, int K, int prio, int dom, bool lab, bool f53, const PersistArgs &a, size_t lds,
-                          hipStream_t score_stream, hipStream_t commit_stream) {
-    if (a.B > 64 || a.B > a.G || a.G < 1) return hipErrorInvalidValue;
-    // the commit workgroup first: it must be resident before the score grid fills the other CUs
-    hipError_t e = launch_persist_commit(K, prio, dom, lab, f53, a, commit_stream);
+                          hipStream_t score_stream, hipStream_t commit_stream, hipStream_t merge_stream) {
+    if (a.B > 64 || a.G < 1) return hipErrorInvalidValue;
+    // check the residency budget before anything is launched (InvalidValue: the caller falls back)
+    hipError_t e = persist_grid(KC, K, prio, dom, lab, f53, a, lds, score_stream, merge_stream, false);
     if (e != hipSuccess) return e;
-    KSCHED_DISPATCH(prio, dom, lab, f53, (persist_kc<P_, D_, L_, F_>(KC, K, a, lds, score_stream)));
+    // the commit workgroup first: it must be resident before the score grid fills the other CUs
+    e = launch_persist_commit(K, prio, dom, lab, f53, a, commit_stream);
+    if (e != hipSuccess) return e;
+    return persist_grid(KC, K, prio, dom, lab, f53, a, lds, score_stream, merge_stream, true);
 }
 
 }  // namespace ksched
