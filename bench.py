@@ -25,20 +25,30 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-leve
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec
 BYTES_PER_PAIR = 24          # node alloc cpu/mem/pods int64 re-read per pod (sequential semantics)
 FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-score pair
-# PMC summary of the same workload (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ passes)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json")
+# PMC summaries of the same workloads (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ
+# passes of `bench.py` itself); keyed by (kernel, config, batch, ranks)
+PMC_SUMMARIES = {
+    ("k_persist_score", "c4", 64, 1): os.path.join(ROOT, "profiles", "r02_pmc_c4_persist.json"),
+    ("k_score_topk", "c4", 64, 1): os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json"),
+}
 
 
-def pmc_traffic(kernel, config, batch):
-    """HBM-side bytes per launch of `kernel` from the committed PMC passes, when they were taken on
-    this workload (c4, the same batch); else None."""
-    if config != "c4" or batch != 64 or not os.path.exists(PMC_SUMMARY):
-        return None, None
-    with open(PMC_SUMMARY) as f:
+def pmc_summary(kernel, config, batch, world):
+    """HBM-side bytes per launch of `kernel` (FETCH_SIZE + WRITE_SIZE) and its VALU occupancy from the
+    committed PMC passes, when they were taken on this workload; else None."""
+    path = PMC_SUMMARIES.get((kernel, config, batch, world))
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
         k = json.load(f)["kernels"].get(kernel)
     if not k or "fabric_bytes_per_launch" not in k:
-        return None, None
-    return k["fabric_bytes_per_launch"], k.get("valu_issue_frac")
+        return None
+    out = {"traffic": k["fabric_bytes_per_launch"], "traffic_source": os.path.relpath(path, ROOT),
+           "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE)"}
+    for f in ("hbm_gbs", "valu_busy_frac", "fp64_issue_frac"):
+        if f in k:
+            out[f"pmc_{f}"] = k[f]
+    return out
 
 
 def parse():
@@ -151,12 +161,22 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    pipeline = eng.stats()["pipeline"]
+    persistent = pipeline == "persistent"
+    # the persistent pipeline is ONE score-grid launch per step: its HIP events (on the grid's own
+    # stream) cost nothing per batch, so the roofline's launch durations come from the timed steps
+    # themselves.  The stream pipeline samples per-batch events in one extra untimed pass instead.
+    if persistent:
+        eng.set_timing(True, 1)
+    step_stats = []
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
+        if persistent:
+            step_stats.append(eng.stats())
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -168,26 +188,43 @@ def main():
     ms = elapsed * 1000.0 / args.steps
     pairs = cl.n_pods * cl.n_nodes
     value = pairs * args.steps / elapsed
-    st_timed = eng.stats()
-    # one more (untimed) pass with sampled per-kernel HIP events on the engine's streams: the
-    # roofline's per-launch durations come from here, not from inside the timed region
-    eng.set_timing(True, 8)
-    step()
-    kstats = [eng.stats()]
-    eng.set_timing(False)
-    st = st_timed
-    # dominant kernel family by timed device time (sampled batches)
-    names = ["k_exact" if mode == MODE_EXACT else "k_score_topk", "k_merge", "k_commit", "rccl_allgather+merge"]
+    st = step_stats[-1] if step_stats else eng.stats()
+    if persistent:
+        eng.set_timing(False)
+        kstats = step_stats
+    else:
+        eng.set_timing(True, 8)
+        step()
+        kstats = [eng.stats()]
+        eng.set_timing(False)
+    names = (["k_exact"] if mode == MODE_EXACT else ["k_persist_score" if persistent else "k_score_topk"]) + \
+        ["k_merge", "k_commit", "rccl_allgather+merge"]
     fam_ms = [sum(s["kernel_ms"][f] for s in kstats) for f in range(4)]
     fam_n = [sum(s["kernel_launches"][f] for s in kstats) for f in range(4)]
-    dom = int(np.argmax([fam_ms[f] / max(fam_n[f], 1) * (st["batches"] if mode == MODE_BATCHED else 1) for f in range(4)]))
     score_pairs = sum(s["kernel_pairs"][0] for s in kstats)
     score_avg_ms = fam_ms[0] / max(fam_n[0], 1)
     score_pairs_per_launch = score_pairs / max(fam_n[0], 1)
     achieved_gbs = score_pairs_per_launch * BYTES_PER_PAIR / (score_avg_ms * 1e-3) / 1e9 if score_avg_ms > 0 else 0.0
-    traffic, valu_frac = pmc_traffic(names[0], args.config, int(eng.opts.batch) or 8 * args.topk)
-    fam_share = {names[f]: (fam_ms[f] / max(fam_n[f], 1)) for f in range(4)}
+    pmc = pmc_summary(names[0], args.config, int(eng.opts.batch) or 8 * args.topk, world)
+    fam_share = {names[f]: (fam_ms[f] / max(fam_n[f], 1)) for f in range(4) if fam_n[f]}
     placed = int(st["placed"])
+    roof = {
+        "kernel": names[0],
+        "bound": "hbm",
+        "achieved": achieved_gbs,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved_gbs / HBM_PEAK_GBS,
+        "traffic": pmc.get("traffic") if pmc else None,
+        "algorithmic_bytes_per_pair": BYTES_PER_PAIR,
+        "pairs_per_launch": score_pairs_per_launch,
+        "avg_launch_ms": score_avg_ms,
+        "launches_timed": fam_n[0],
+        "timing": "HIP events on the score grid's stream, inside the timed steps" if persistent else
+                  "HIP events on the score stream, one batch in 8 of one untimed pass",
+    }
+    if pmc:
+        roof.update({k: v for k, v in pmc.items() if k != "traffic"})
     out = {
         "metric": "pod-node evaluations/sec",
         "value": value,
@@ -205,31 +242,17 @@ def main():
                                f"{'resource (balanced+least-requested)' if cl.priority == 0 else 'best-price'} priority, "
                                f"{'feasible-only' if cl.domain else 'all-node'} argmax, labels={bool(cl.use_labels)}",
                    "nodes": cl.n_nodes, "pods": cl.n_pods, "mode": args.mode, "topk": args.topk,
-                   "batch": int(eng.opts.batch) or 8 * args.topk, "parallelism": f"node-shard x{world}"},
+                   "batch": int(eng.opts.batch) or 8 * args.topk, "parallelism": f"node-shard x{world}",
+                   "pipeline": pipeline},
         "pods_per_sec": cl.n_pods * args.steps / elapsed,
         "placed_pods": placed,
+        "placed_pods_per_sec": placed * args.steps / elapsed,
         "batches_per_step": int(st["batches"]),
         "truncated_batches_per_step": int(st["truncations"]),
         "kernel_avg_ms": fam_share,
-        "roofline": {
-            "kernel": names[0],
-            "bound": "hbm",
-            "achieved": achieved_gbs,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved_gbs / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc_c4_b64.json)",
-            "valu_issue_frac_pmc": valu_frac,
-            "algorithmic_bytes_per_pair": BYTES_PER_PAIR,
-            "pairs_per_launch": score_pairs_per_launch,
-            "avg_launch_ms": score_avg_ms,
-            "fp64_tflops_equiv": score_pairs_per_launch * FLOPS_PER_PAIR / (score_avg_ms * 1e-3) / 1e12 if score_avg_ms > 0 else 0.0,
-            "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
-            "dominant_family": names[dom],
-        },
+        "roofline": roof,
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base, mt = cpu_baseline(cl, args.cpu_baseline_s)
         out["cpu_baseline"] = base
         if mt:

@@ -634,7 +634,7 @@ __global__ __launch_bounds__(kSpcThreads) __attribute__((amdgpu_num_vgpr(96))) v
 // batch.  It waits for the B merges of an active batch (Ctl::merged, sc1 poll), commits it exactly as
 // k_commit_spc does (lists read with sc1 loads; export, plans and cursor left as sc1 stores) and
 // publishes Ctl::committed.  Once every pod is resolved it publishes a committed count no wait can
-// exceed, so every score workgroup still waiting can see the end.  Every wait is bounded (2 s).
+// exceed, so every score workgroup still waiting can see the end.  Every wait is bounded (KSCHED_PERSIST_TIMEOUT_MS).
 // It runs alone on the CU the score grid leaves free, so it is not capped below 256 VGPRs.
 // ------------------------------------------------------------------------------------------------
 template <int K, int PRIO, int DOM, bool LAB, bool F53>

@@ -575,7 +575,9 @@ int enqueue_persistent(ksched_ctx *c) {
     a.xbuf_bytes = (int64_t)xb;
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     a.err = c->d_err;
-    a.timeout_ticks = 200000000;  // 2 s of the 100 MHz wall clock
+    // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
+    // queues for a while must not turn into a spurious timeout)
+    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
     if (env_int("KSCHED_PERSIST_TRACE", 0)) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {
@@ -606,10 +608,19 @@ int enqueue_persistent(ksched_ctx *c) {
     HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit and merge streams start after the initialisation
     HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
     HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
+    // timing: the score grid's launch (family 0) is bracketed by events on ITS stream -- one launch per
+    // call, so the events cost nothing per batch and may stay on inside a timed region
+    int e0 = -1;
+    HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, sS));
     const hipError_t e =
         launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC, sM);
-    if (e == hipErrorInvalidValue) return 1;  // does not fit after all: the stream pipeline runs
+    if (e == hipErrorInvalidValue) {  // does not fit after all: the stream pipeline runs
+        c->timed.clear();
+        c->ev_used = 0;
+        return 1;
+    }
     if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("launch_persist: ") + hipGetErrorString(e));
+    HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n, sS));
     HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));  // the run's end event on stream S covers commit + merge
     HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
     HIPCHK(c, hipEventRecord(c->ev_pipe[2], sM));

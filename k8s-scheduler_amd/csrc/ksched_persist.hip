@@ -16,7 +16,7 @@
 //
 // Every hand-off is MI355X_MICROARCH "valid forms" row 1: sc1 stores of the handed-off bytes, every
 // storing wave drained, ONE lane's counter update (atomic add / flag store), sc1 loads after the poll
-// -- no L2 write-back fences.  Every wait is bounded (2 s -> error word 5).
+// -- no L2 write-back fences.  Every wait is bounded (KSCHED_PERSIST_TIMEOUT_MS, default 10 s -> error words 5..9).
 // Snapshot semantics are the stream pipeline's (score(b) sees every commit up to b-2, commit(b)
 // inherits b-1's), so results are bit-identical; tests/test_gpu_parity.py runs both.
 #include <hip/hip_runtime.h>

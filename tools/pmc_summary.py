@@ -7,12 +7,15 @@ Each DIR holds a `run_counter_collection.csv` from `rocprofv3 --pmc ... --kernel
 --output-format csv -o run`.  For every pipeline kernel family (score / merge / commit) the output
 holds the per-launch average of every counter, the launch count and the average profiled duration.
 Derived (MI355X_MICROARCH.md "HBM" + "rocprofv3 PMC slots"):
-  fabric_bytes_per_launch = (FETCH_SIZE + WRITE_SIZE) * 1024  (both counters are in KiB; no x2
-      correction for FETCH_SIZE: the score kernel's row loads are wave-uniform, not 16 B/lane
-      streams, and the measured fetch equals one pass over the 96 B node rows)
-  valu_issue_frac = SQ_INSTS_VALU / (profiled duration * 256 CU * clock), one VALU wave-instruction
-      per CU per clock being the FP64 issue peak (78.6 TFLOP/s = 256 CU x 2.4 GHz x 64 FMA lanes)
-bench.py reads the file to fill roofline.traffic.
+  fabric_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  (both counters are in KiB; on
+      gfx950 FETCH_SIZE reports half the bytes of a coalesced read, MI355X_MICROARCH.md "HBM")
+  A wave64 VALU instruction occupies its SIMD (16 FP64 lanes, 32 FP32/INT lanes on gfx950) for 4
+  cycles when it is FP64 (ADD/MUL/FMA/TRANS_F64; 78.6 TFLOP/s = 1024 SIMD x 16 lanes x 2 x 2.4 GHz)
+  and 2 cycles otherwise, so over a launch of duration T on 1024 SIMDs:
+  valu_busy_frac  = (4 * f64 + 2 * (VALU - f64)) / (T * 1024 SIMD * clock)   -- VALU pipe occupancy
+  fp64_issue_frac = 4 * f64 / (T * 1024 * clock)                             -- FP64 share of that
+  hbm_gbs         = fabric bytes / T
+bench.py reads the file to fill roofline.traffic and the VALU fields.
 """
 import csv
 import json
@@ -20,10 +23,13 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILIES = {"k_score_topk": "score", "k_merge_pod": "merge", "k_merge": "merge", "k_commit": "commit",
+FAMILIES = {"k_persist_score": "score", "k_persist_merge": "merge", "k_persist_commit": "commit",
+            "k_score_topk": "score", "k_merge_pod": "merge", "k_merge": "merge", "k_commit": "commit",
             "k_exact": "exact"}
 CUS = 256
+SIMDS = 4 * CUS
 CLOCK_HZ = 2.4e9
+F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")
 
 
 def family(name):
@@ -58,13 +64,18 @@ def main():
         if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
             k["fetch_bytes_per_launch"] = avg["FETCH_SIZE"] * 1024
             k["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024
-            k["fabric_bytes_per_launch"] = (avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
-        if "SQ_INSTS_VALU" in avg and dur_ns > 0:
-            k["valu_issue_frac"] = avg["SQ_INSTS_VALU"] / (dur_ns * 1e-9 * CUS * CLOCK_HZ)
-        f64 = sum(avg.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
-                                            "SQ_INSTS_VALU_TRANS_F64"))
+            k["fabric_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        f64 = sum(avg.get(c, 0.0) for c in F64)
         if f64:
             k["f64_valu_insts_per_launch"] = f64
+        if dur_ns > 0:
+            cyc = dur_ns * 1e-9 * SIMDS * CLOCK_HZ
+            if "fabric_bytes_per_launch" in k:
+                k["hbm_gbs"] = k["fabric_bytes_per_launch"] / dur_ns
+            if f64:
+                k["fp64_issue_frac"] = 4 * f64 / cyc
+                if "SQ_INSTS_VALU" in avg:  # from the same run only when both groups were in one pass
+                    k["valu_busy_frac"] = (4 * f64 + 2 * (avg["SQ_INSTS_VALU"] - f64)) / cyc
         res["kernels"][kern] = k
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
