@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--no-check", action="store_true",
                     help="skip the (untimed) prefix check of the timed run's results against the CPU oracle")
     ap.add_argument("--check-pods", type=int, default=5000)
+    ap.add_argument("--no-xchg", action="store_true", help="N > 1: RCCL stream pipeline instead of the device-side exchange")
+    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # N > 1 rehearsal on one GPU
     return ap.parse_args()
 
 
@@ -134,19 +136,31 @@ def main():
     if world != args.gpus and args.gpus > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dist = None
+    if args.same_device:
+        # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, each grid on its share of
+        # the CUs, torch.distributed over gloo, no RCCL communicator (RCCL refuses two ranks per GPU)
+        local = 0
+        os.environ.setdefault("KSCHED_PERSIST_G", str(max(8, (256 - 8 * world) // world // 8 * 8)))
+    tdev = "cpu" if args.same_device else "cuda"
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.same_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import torch
 
     cl = cluster.make_cluster(args.config, n_nodes=args.nodes, n_pods=args.pods)
     mode = MODE_EXACT if args.mode == "exact" else MODE_BATCHED
     if world > 1 and mode == MODE_EXACT:
         mode = MODE_BATCHED
+    # N > 1: the persistent pipeline with the device-side exchange over xGMI (ksched_xchg_*), the RCCL
+    # communicator kept as the fallback transport (stream pipeline, one all-gather per batch)
     eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=local, mode=mode, topk=args.topk,
-                                        batch=args.batch, timing=False)
+                                        batch=args.batch, timing=False, xchg=world > 1 and not args.no_xchg,
+                                        comm=not args.same_device)
     eng.save_state()
     eng.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
 
@@ -159,8 +173,24 @@ def main():
         eng.sync()
         return eng.results()
 
-    for _ in range(args.warmup):
-        step()
+    for w in range(max(args.warmup, 1 if world > 1 else 0)):
+        if world > 1 and w == 0:
+            # every rank must take the same transport: if the exchange failed anywhere (a device
+            # timeout), all ranks fall back to the RCCL stream pipeline together
+            from ksched import KschedError
+            ok = 1
+            try:
+                step()
+            except KschedError as ex:
+                ok = 0
+                print(f"rank {rank}: device-side exchange failed ({ex}); falling back to RCCL", file=sys.stderr)
+            t = torch.tensor([ok], dtype=torch.int32, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if int(t.item()) == 0:
+                os.environ["KSCHED_XCHG"] = "0"
+                step()
+        else:
+            step()
     pipeline = eng.stats()["pipeline"]
     persistent = pipeline == "persistent"
     # the persistent pipeline is ONE score-grid launch per step: its HIP events (on the grid's own
@@ -182,7 +212,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed * 1000.0 / args.steps
@@ -243,7 +273,8 @@ def main():
                                f"{'feasible-only' if cl.domain else 'all-node'} argmax, labels={bool(cl.use_labels)}",
                    "nodes": cl.n_nodes, "pods": cl.n_pods, "mode": args.mode, "topk": args.topk,
                    "batch": int(eng.opts.batch) or 8 * args.topk, "parallelism": f"node-shard x{world}",
-                   "pipeline": pipeline},
+                   "pipeline": pipeline, "transport": ("xgmi-rings" if pipeline == "persistent" else "rccl-allgather")
+                                                       if world > 1 else "none"},
         "pods_per_sec": cl.n_pods * args.steps / elapsed,
         "placed_pods": placed,
         "placed_pods_per_sec": placed * args.steps / elapsed,

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 2
+#define KSCHED_ABI_VERSION 3
 
 /* status codes */
 #define KSCHED_OK 0
@@ -121,6 +121,22 @@ int ksched_set_comm(ksched_ctx *ctx, const uint8_t id[128]);
  * GPU (a test vehicle, one host round trip per batch); contexts set opts.rank / nranks / node_offset /
  * nodes_global as for ksched_set_comm, call ksched_set_group instead of it, and must run the same
  * schedule calls concurrently. */
+/* Device-side candidate exchange for the node-sharded batched path (one process per GPU, 2..8 ranks,
+ * batch <= 64): instead of one RCCL all-gather per batch launched from the host, the persistent
+ * pipeline's merger workgroups write each pod's candidate list straight into every rank's receive
+ * ring over xGMI (tagged 8-byte granules in uncached device memory) and rank-merge the R lists they
+ * receive -- no launch, no host round trip, no collective per batch.  Setup, on every rank:
+ *   ksched_xchg_export(ctx, h)          allocates this rank's ring; h = its IPC handle
+ *   (all-gather the R handles in rank order, e.g. torch.distributed)
+ *   ksched_xchg_import(ctx, handles)    maps every rank's ring (R * 64 bytes, own entry ignored)
+ * Batched runs then take the exchange path on every rank (an RCCL communicator is optional: it is
+ * the fallback when a device timeout disables the exchange; ksched_xchg_ready reports the state).
+ * Replaces the same all-gather as ksched_set_comm; the call sequence is unchanged. */
+#define KSCHED_XCHG_HANDLE_BYTES 64
+int ksched_xchg_export(ksched_ctx *ctx, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]);
+int ksched_xchg_import(ksched_ctx *ctx, const uint8_t *handles);
+int ksched_xchg_ready(const ksched_ctx *ctx);
+
 typedef struct ksched_group ksched_group;
 int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out);
 int ksched_group_destroy(ksched_group *g); /* after every context using it is destroyed */

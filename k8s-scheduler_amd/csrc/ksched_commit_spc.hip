@@ -202,21 +202,39 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
     const int64_t fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
     const int cut0 = (wave == 0 && pj) ? load_rec<COH>(A.lists + (size_t)lane * K).pad : 0;
 
+    // every thread's list entries: only their (key, idx | valid) words, all loads in flight at once,
+    // issued before the table initialisation so their latency overlaps it
+    constexpr int kHeadPer = (64 * K + kSpcThreads - 1) / kSpcThreads;
+    uint64_t w0[kHeadPer], w1[kHeadPer];
+#pragma unroll
+    for (int u = 0; u < kHeadPer; ++u) {
+        const int e = tid + u * kSpcThreads;
+        w0[u] = 0; w1[u] = 0;  // valid = 0
+        if (e < 64 * K && e / K < nb) {
+            const uint64_t *w = reinterpret_cast<const uint64_t *>(A.lists + e);
+            if (COH) { w0[u] = ld_coh(w); w1[u] = ld_coh(w + 1); }
+            else { w0[u] = w[0]; w1[u] = w[1]; }
+        }
+    }
+
     // ---- prologue (all waves) ----
     for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
-    for (int e = tid; e < 64 * K; e += kSpcThreads) {
-        const int j = e / K, q = e % K;
-        double key = -__builtin_inf();
-        int32_t idx = kNoIdx;
-        if (j < nb) {
-            const Rec r = load_rec<COH>(A.lists + e);
-            if (r.valid) { key = r.key; idx = r.idx; }
+    {
+#pragma unroll
+        for (int u = 0; u < kHeadPer; ++u) {
+            const int e = tid + u * kSpcThreads;
+            if (e < 64 * K) {
+                const int j = e / K, q = e % K;
+                const bool v = (uint32_t)(w1[u] >> 32) != 0;
+                const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
+                const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
+                m.LK[q * 64 + j] = key;
+                m.LI[q * 64 + j] = idx;
+                m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
+            }
         }
-        m.LK[q * 64 + j] = key;
-        m.LI[q * 64 + j] = idx;
-        m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
     }
     const int nin = COH ? L->xcount : A.xin->count;  // <= 64
     for (int e = tid; e < nin; e += kSpcThreads) {

@@ -123,6 +123,14 @@ struct ksched_ctx {
     size_t pws_bytes = 0;
     bool persist_stats = false;  // stats come from the Ctl copy queued behind the run
     int64_t persist_B = 0;
+    // device-side candidate exchange of the node-sharded persistent pipeline (ksched_xchg_*)
+    void *d_rx = nullptr;          // this rank's receive ring (uncached device memory)
+    size_t rx_bytes = 0;
+    char *rx_peer[kMaxXchgRanks] = {};  // every rank's ring as mapped here (own = d_rx)
+    bool xchg_ready = false;       // rings imported: batched runs take the persistent multi-rank path
+    bool xchg_run = false;         // the current run uses the exchange
+    uint32_t xchg_epoch = 1;       // granule tag base of the next call (identical on every rank)
+    int32_t *d_xmin = nullptr;     // k_xchg_min result
 };
 
 namespace {
@@ -243,6 +251,17 @@ BatchPlan plan_batch(const ksched_ctx *c) {
 }
 
 
+// The exchange fields of PersistArgs (node-sharded persistent pipeline; R > 1).
+void fill_xchg_args(const ksched_ctx *c, PersistArgs *a) {
+    a->B = c->B;
+    a->node_offset = c->o.node_offset;
+    a->R = c->xchg_run ? c->o.nranks : 1;
+    a->rank = c->xchg_run ? c->o.rank : 0;
+    a->epoch0 = c->xchg_epoch;
+    a->xchg_stride = (int64_t)xchg_stride_bytes(c->K);
+    for (int r = 0; r < kMaxXchgRanks; ++r) a->rx_peer[r] = c->rx_peer[r];
+}
+
 // fast53 for this call: every |alloc| + sum of |requests| < 2^52, on every rank.
 int decide_fast53(ksched_ctx *c) {
     int flag = sat_add(c->max_abs_alloc, c->sum_abs_req) < (1ull << 52) ? 1 : 0;
@@ -250,6 +269,22 @@ int decide_fast53(ksched_ctx *c) {
     if (c->group) {
         int mn = flag;
         if (!group_min(c->group, flag, &mn)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer never called run");
+        flag = mn;
+    } else if (c->xchg_run) {
+        // the ranks meet on the device through their rings (no collective launch)
+        PersistArgs a{};
+        fill_xchg_args(c, &a);
+        a.err = c->d_err;
+        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
+        int32_t mn = -1;
+        HIPCHK(c, launch_xchg_min(a, flag, c->d_xmin, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&mn, c->d_xmin, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (mn < 0) {
+            c->xchg_ready = false;
+            hipMemset(c->d_err, 0, sizeof(int32_t));
+            return fail(c, KSCHED_E_DEVICE, "node-sharded exchange: a peer rank never met this one (device barrier timed out)");
+        }
         flag = mn;
     } else if (c->comm) {
         int32_t *d = c->d_err;  // scratch word (zeroed again before use by exact mode)
@@ -535,17 +570,21 @@ constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
 
 int enqueue_persistent(ksched_ctx *c) {
     if (env_int("KSCHED_PERSIST", 1) == 0) return 1;
-    if (c->comm || c->group || c->o.nranks > 1 || c->o.node_offset != 0) return 1;
+    // single rank, or node-sharded with the device-side exchange (the RCCL / in-process group paths
+    // run the stream pipeline)
+    if (!c->xchg_run && (c->comm || c->group || c->o.nranks > 1 || c->o.node_offset != 0)) return 1;
     const int K = c->K, KC = c->KC, B = c->B;
     if (B > 64 || KC > 8 || (c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL)) return 1;
     const int64_t n = c->n_local;
+    // node-sharded: every rank sizes its grid for the largest shard, so all ranks take the same path
+    const int64_t n_geom = c->xchg_run ? std::max<int64_t>(n, (c->n_global + c->o.nranks - 1) / c->o.nranks) : n;
     // workgroups of a launch go round-robin to the 8 XCDs (32 CUs each), so the grid must leave one CU
     // free on EVERY XCD for the commit workgroup to be guaranteed a place: G <= CUs - 8 (measured: with
     // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts)
     const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - kXcds));
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n + 15) / 16));
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n_geom + 15) / 16));
     if (G > c->cus - kXcds) return 1;
-    const int R = (int)((n + G - 1) / G);
+    const int R = (int)((n_geom + G - 1) / G);
     const size_t lds = persist_score_lds(KC, R);
     if (lds == 0) return 1;
     // workspace: part lists [2][B][G][KC] + counts [2][B][G], list ring 4 x (B*K Rec + B fc), XBuf ring
@@ -574,6 +613,8 @@ int enqueue_persistent(ksched_ctx *c) {
     a.xring = a.lring + 4 * lists_b;
     a.xbuf_bytes = (int64_t)xb;
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
+    fill_xchg_args(c, &a);
+    a.merge_low_prio = env_int("KSCHED_MERGE_LOW_PRIO", 0);
     a.err = c->d_err;
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)
@@ -764,7 +805,10 @@ int ksched_destroy(ksched_ctx *c) {
     }
     for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
-    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace);
+    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_xmin);
+    for (int r = 0; r < kMaxXchgRanks; ++r)
+        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx) hipIpcCloseMemHandle(c->rx_peer[r]);
+    hipFree(c->d_rx);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
     if (c->stream3) hipStreamDestroy(c->stream3);
@@ -830,6 +874,53 @@ int ksched_set_group(ksched_ctx *c, ksched_group *g) {
     c->group = g;
     return KSCHED_OK;
 }
+
+int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) {
+    if (!c || !handle) return KSCHED_E_INVALID;
+    const int R = c->o.nranks;
+    if (R < 2 || R > kMaxXchgRanks) return fail(c, KSCHED_E_INVALID, "xchg_export: 2 <= nranks <= 8");
+    if (c->B > 64) return fail(c, KSCHED_E_INVALID, "xchg_export: the persistent pipeline needs batch <= 64");
+    if (c->group) return fail(c, KSCHED_E_STATE, "xchg_export: context uses an in-process rank group");
+    HIPCHK(c, hipSetDevice(c->dev));
+    const size_t bytes = xchg_ring_bytes(R, c->B, c->K);
+    if (!c->d_rx) {
+        // uncached: a peer's xGMI stores and this GPU's polls meet in memory, never in a stale L2 line
+        HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
+        HIPCHK(c, hipMemset(c->d_rx, 0, bytes));  // tag 0 is never a live tag (epochs start at 1)
+        c->rx_bytes = bytes;
+    }
+    if (!c->d_xmin) HIPCHK(c, hipMalloc((void **)&c->d_xmin, sizeof(int32_t)));
+    hipIpcMemHandle_t h;
+    HIPCHK(c, hipIpcGetMemHandle(&h, c->d_rx));
+    static_assert(sizeof(hipIpcMemHandle_t) == KSCHED_XCHG_HANDLE_BYTES, "ipc handle size");
+    std::memcpy(handle, &h, sizeof(h));
+    return KSCHED_OK;
+}
+
+int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
+    if (!c || !handles) return KSCHED_E_INVALID;
+    if (!c->d_rx) return fail(c, KSCHED_E_STATE, "xchg_import before xchg_export");
+    HIPCHK(c, hipSetDevice(c->dev));
+    const int R = c->o.nranks;
+    for (int r = 0; r < kMaxXchgRanks; ++r) {
+        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx) hipIpcCloseMemHandle(c->rx_peer[r]);
+        c->rx_peer[r] = nullptr;
+    }
+    c->xchg_ready = false;
+    for (int r = 0; r < R; ++r) {
+        if (r == c->o.rank) { c->rx_peer[r] = static_cast<char *>(c->d_rx); continue; }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES, sizeof(h));
+        void *p = nullptr;
+        HIPCHK(c, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        c->rx_peer[r] = static_cast<char *>(p);
+    }
+    c->xchg_ready = true;
+    c->xchg_epoch = 1;
+    return KSCHED_OK;
+}
+
+int ksched_xchg_ready(const ksched_ctx *c) { return c && c->xchg_ready ? 1 : 0; }
 
 int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t *am, const int64_t *ap,
                       const uint64_t *labels, const float *price) {
@@ -1114,12 +1205,13 @@ int ksched_run(ksched_ctx *c) {
     c->timed.clear();
     c->ev_used = 0;
     c->st.pods = c->p;
+    int mode = c->o.mode;
+    if (mode == KSCHED_MODE_AUTO) mode = c->o.nranks > 1 ? KSCHED_MODE_BATCHED : KSCHED_MODE_EXACT;
+    c->xchg_run = c->xchg_ready && mode == KSCHED_MODE_BATCHED && c->p > 0 && env_int("KSCHED_XCHG", 1) != 0;
     if (int rr = decide_fast53(c)) return rr;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int r = KSCHED_OK;
     if (c->p > 0) {
-        int mode = c->o.mode;
-        if (mode == KSCHED_MODE_AUTO) mode = c->o.nranks > 1 ? KSCHED_MODE_BATCHED : KSCHED_MODE_EXACT;
         c->persist_stats = false;
         if (mode == KSCHED_MODE_EXACT) {
             r = enqueue_exact(c);
@@ -1127,7 +1219,11 @@ int ksched_run(ksched_ctx *c) {
         } else {
             r = enqueue_persistent(c);
             c->st.pipeline = KSCHED_PIPE_PERSISTENT;
+            if (r == 1 && c->xchg_run && !c->comm)
+                r = fail(c, KSCHED_E_INVALID, "node-sharded exchange: the persistent pipeline does not fit this "
+                                              "configuration and no RCCL communicator is set");
             if (r == 1) {  // not eligible: the stream pipeline
+                c->xchg_run = false;
                 r = enqueue_batched(c);
                 c->st.pipeline = c->B > 64 || c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL ? KSCHED_PIPE_STREAM_SEQ
                                                                                           : KSCHED_PIPE_STREAM;
@@ -1172,6 +1268,18 @@ int ksched_sync(ksched_ctx *c) {
     }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
+    if (c->xchg_run) {
+        // every rank counted the same active batches: the next call's tags start past this call's
+        const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+        c->xchg_epoch += (uint32_t)h->nact + 2u;
+        if (e) c->xchg_ready = false;  // the rings' state is unknown: later calls take the RCCL path
+        c->xchg_run = false;
+    }
+    if (e == 10 || e == 11) {
+        hipMemset(c->d_err, 0, sizeof(int32_t));
+        return fail(c, KSCHED_E_DEVICE, e == 10 ? "node-sharded exchange: a merger's wait for a peer rank's candidate lists timed out"
+                                                : "node-sharded exchange: the device barrier timed out");
+    }
     if (e >= 5 && e <= 9) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
         static const char *what[] = {"the commit's wait for the merges", "a score workgroup's wait for commit(b-2)",

@@ -102,6 +102,7 @@ struct alignas(8) Ctl {
     unsigned long long arrive[4];  // score workgroups done with active batch a: G per use of the slot
     unsigned long long merged[4];  // merger workgroups done with active batch a: B per use of the slot
     int64_t cursor_at[kPlanRing];  // cursor right after commit(b), slot b % kPlanRing
+    int64_t nact;                  // persistent pipeline: active batches of the call (merger 0)
 };
 
 struct PodArgs {
@@ -170,7 +171,14 @@ struct MergeArgs {
     const unsigned long long *wait_ctr;  // k_merge_pod: poll until *wait_ctr >= wait_target (null: no wait)
     unsigned long long wait_target;
     int32_t *err;                        // device error word (2 = the wait timed out)
+    uint32_t *lds_msg;                   // non-null: the final list goes to LDS as a PodMsg (kMsgWords)
+    int32_t low_prio;                    // 1: merge waves at issue priority 0 (persistent mergers, A/B)
 };
+
+// One pod's merged candidate list as 32-bit words, the unit the ranks exchange in the persistent
+// multi-rank pipeline: K Rec rows (14 words each, the Rec layout) then the feasible count (2 words).
+constexpr int kRecWords = (int)(sizeof(Rec) / 4);
+constexpr int msg_words(int K) { return K * kRecWords + 2; }
 
 // The persistent commit workgroup's private control state (LDS): it is the only writer of the plans,
 // the cursor, the stats and the export once its kernel runs, so it reads its own copies instead of
@@ -338,7 +346,23 @@ struct PersistArgs {
     int64_t trace_cap;
     int64_t *cdbg;  // KSCHED_COMMIT_STAMPS: commit phase cycle sums (CommitArgs::dbg), else null
     int64_t *mdbg;  // KSCHED_MERGE_STAMPS: merge phase cycle sums (MergeArgs::dbg), else null
+    // node-sharded (R > 1, one process per GPU): this rank owns global nodes [node_offset, +n_local);
+    // merger m of every rank writes pod m's list into EVERY rank's receive ring (rx_peer[r], slot
+    // (active batch % 4, source rank, pod) of xchg_stride bytes) as tagged 8-byte granules {word, tag},
+    // then gathers the R lists of pod m from its own ring and rank-merges them (ksched_persist.hip)
+    int64_t node_offset;
+    int32_t R, rank;
+    uint32_t epoch0;        // granule tag of this call's active batch a is epoch0 + a (a >= 1)
+    int64_t xchg_stride;    // bytes per pod message in a ring
+    char *rx_peer[8];       // every rank's receive ring, mapped into this process (rx_peer[rank] = own)
+    int32_t merge_low_prio; // KSCHED_MERGE_LOW_PRIO: mergers yield issue slots to the score waves
 };
+constexpr int kMaxXchgRanks = 8;
+// receive ring: [4 active-batch slots][R source ranks][B pods] messages, then R barrier granules
+constexpr size_t xchg_stride_bytes(int K) { return ((size_t)msg_words(K) * 8 + 63) / 64 * 64; }
+constexpr size_t xchg_ring_bytes(int R, int B, int K) { return (size_t)4 * R * B * xchg_stride_bytes(K) + 64 * (size_t)R; }
+// all ranks meet on the device and agree on the minimum of a small value (tag: this call's epoch0)
+hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hipStream_t s);
 // trace columns: score start (WG 0 past its wait), last arrival, last merge done, commit start, commit end
 constexpr int kTraceCols = 16;
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {

@@ -861,6 +861,7 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     ctl->committed = 0;
     for (int i = 0; i < 4; ++i) { ctl->arrive[i] = 0; ctl->merged[i] = 0; }
     for (int i = 0; i < kPlanRing; ++i) ctl->cursor_at[i] = 0;
+    ctl->nact = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;
     ctl->plan[0] = P > 0 ? 0 : -1;
     ctl->plan[1] = B < P ? B : -1;

@@ -57,7 +57,8 @@ __device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb
 
 template <int KC, int K, bool COH = false>
 __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
-    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    // latency-critical: win issue arbitration over co-resident score waves (low_prio: yield to them)
+    if (A.low_prio) __builtin_amdgcn_s_setprio(0); else __builtin_amdgcn_s_setprio(3);
     constexpr int W = kMergeThreads / 64;
     __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
     __shared__ int32_t s_idx[kMergeThreads][KC];
@@ -215,9 +216,22 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
             r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
         }
         r.pad = lane == 0 ? cut_out : 0;
-        store_rec<COH>(A.out_rec + (size_t)b * K + lane, r);
+        if (A.lds_msg) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(&r);
+#pragma unroll
+            for (int x = 0; x < kRecWords; ++x) A.lds_msg[lane * kRecWords + x] = w[x];
+        } else {
+            store_rec<COH>(A.out_rec + (size_t)b * K + lane, r);
+        }
     }
-    if (lane == 0) store_i64<COH>(A.out_fc + b, gcnt);
+    if (lane == 0) {
+        if (A.lds_msg) {
+            A.lds_msg[K * kRecWords] = (uint32_t)(uint64_t)gcnt;
+            A.lds_msg[K * kRecWords + 1] = (uint32_t)((uint64_t)gcnt >> 32);
+        } else {
+            store_i64<COH>(A.out_fc + b, gcnt);
+        }
+    }
     if (dbg && lane == 0) {
         ts[6] = __builtin_amdgcn_s_memtime();
         for (int k = 1; k < 7; ++k) atomicAdd((unsigned long long *)&A.dbg[k - 1], (unsigned long long)(ts[k] - ts[k - 1]));

@@ -48,6 +48,87 @@ __device__ __forceinline__ bool spin_ge(const unsigned long long *p, unsigned lo
 // the first failure names the wait that timed out (ksched_sync reports it)
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
+// Cross-device granules: system-scope relaxed 8-byte accesses (global_store/load ... sc0 sc1) on the
+// uncached receive rings; an 8-byte store arrives whole, so a granule whose tag matches holds its word.
+__device__ __forceinline__ void st_sys(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// poll one granule until it carries `tag` (false: timed out)
+__device__ __forceinline__ bool granule_wait(const uint64_t *p, uint32_t tag, int64_t limit, uint32_t *word) {
+    uint64_t v = ld_sys(p);
+    if ((uint32_t)(v >> 32) != tag) {
+        const uint64_t t0 = wall_clock64();
+        do {
+            if ((int64_t)(wall_clock64() - t0) > limit) return false;
+            __builtin_amdgcn_s_sleep(1);
+            v = ld_sys(p);
+        } while ((uint32_t)(v >> 32) != tag);
+    }
+    *word = (uint32_t)v;
+    return true;
+}
+
+// Rank merge of pod m's R exchanged lists (wave 0, lane = source rank; the stream pipeline's
+// k_merge<INPUT_REC> rule): K rounds of wave arg-best over the lists' heads, entries ranking below the
+// best cutoff of a cut list dropped, cut when any input was cut or entries were left over.
+template <int K>
+__device__ __forceinline__ void rank_merge_msgs(const uint32_t *all, int R, Rec *out, int64_t *out_fc) {
+    constexpr int MW = msg_words(K);
+    const int lane = threadIdx.x & 63;
+    const bool has = lane < R;
+    const uint32_t *msg = all + (has ? lane : 0) * MW;
+    auto rec_key = [&](int q) {
+        return __longlong_as_double((long long)(((uint64_t)msg[q * kRecWords + 1] << 32) | msg[q * kRecWords]));
+    };
+    int n = 0;
+    if (has) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) n += msg[q * kRecWords + 3] != 0;  // valid entries form a prefix
+    }
+    const bool cut = has && msg[13] != 0;  // entry 0's pad (Rec word 13)
+    int64_t cnt = has ? (int64_t)(((uint64_t)msg[K * kRecWords + 1] << 32) | msg[K * kRecWords]) : 0;
+    cnt = wave_sum_i64(cnt);
+    double ck = (cut && n > 0) ? rec_key(n - 1) : -__builtin_inf();
+    int32_t ci = (cut && n > 0) ? (int32_t)msg[(n - 1) * kRecWords + 2] : kNoIdx;
+    const bool anycut = __ballot(cut) != 0;
+    {
+        int32_t aux = 0;
+        wave_argbest(ck, ci, aux);
+    }
+    int h = 0;
+    double mk = -__builtin_inf();
+    int32_t mi = kNoIdx, msrc = -1;
+    for (int r = 0; r < K; ++r) {
+        double k = (h < n) ? rec_key(h) : -__builtin_inf();
+        int32_t ix = (h < n) ? (int32_t)msg[h * kRecWords + 2] : kNoIdx;
+        int32_t src = lane * K + h;
+        wave_argbest(k, ix, src);
+        if (ix == kNoIdx) break;  // wave-uniform
+        if (src == lane * K + h) ++h;
+        if (lane == r) { mk = k; mi = ix; msrc = src; }
+    }
+    const bool left = __ballot(h < n) != 0;
+    if (anycut && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
+    const int32_t cut_out = (anycut || left) ? 1 : 0;
+    if (lane < K) {
+        Rec r{};
+        if (mi != kNoIdx) {
+            uint32_t *w = reinterpret_cast<uint32_t *>(&r);
+            const uint32_t *sw = all + (msrc / K) * MW + (msrc % K) * kRecWords;
+#pragma unroll
+            for (int x = 0; x < kRecWords; ++x) w[x] = sw[x];
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        r.pad = lane == 0 ? cut_out : 0;
+        store_rec<true>(out + lane, r);
+    }
+    if (lane == 0) store_i64<true>(out_fc, cnt);
+}
+
 __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int64_t a2) {
     nd->a[0] = a0; nd->a[1] = a1; nd->a[2] = a2;
     const double f0 = (double)a0, f1 = (double)a1, f2 = (double)a2;
@@ -108,8 +189,8 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
             const int nx = (int)(uint32_t)ld_coh(&xb->count);
             for (int e = tid; e < nx; e += kPThreads) {
                 const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
-                const int64_t j = (int64_t)(int32_t)(uint32_t)ld_coh(w);
-                if (j % G != g) continue;
+                const int64_t j = (int64_t)(int32_t)(uint32_t)ld_coh(w) - P.node_offset;  // local row
+                if (j < 0 || j >= n || j % G != g) continue;  // another rank's node, or another workgroup's
                 const int64_t c0 = (int64_t)ld_coh(w + 4), c1 = (int64_t)ld_coh(w + 5), c2 = (int64_t)ld_coh(w + 6);
                 set_row(rows + j / G, c0, c1, c2);
                 // the mergers read a candidate's state from its HBM row (sc1)
@@ -169,7 +250,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
 #pragma unroll
             for (int u = 0; u < kPU; ++u) {
                 double ck = ks[u];
-                int32_t ci = (int32_t)(g + (int64_t)(r0 + u * kPW) * G);
+                int32_t ci = (int32_t)(P.node_offset + g + (int64_t)(r0 + u * kPW) * G);  // global index
                 bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
 #pragma unroll
                 for (int q = 0; q < KC; ++q) {
@@ -249,6 +330,8 @@ template <int KC, int K>
 __global__ __launch_bounds__(kMergeThreads) void k_persist_merge(PersistArgs P) {
     __shared__ int64_t s_p0, s_done;
     __shared__ int s_stop;
+    __shared__ uint32_t s_msg[msg_words(K)];                  // this rank's list of pod m (R > 1)
+    __shared__ uint32_t s_all[kMaxXchgRanks * msg_words(K)];  // every rank's list of pod m
     const int tid = threadIdx.x;
     const int m = blockIdx.x;
     const int G = P.G;
@@ -299,19 +382,82 @@ __global__ __launch_bounds__(kMergeThreads) void k_persist_merge(PersistArgs P) 
         ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
         ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
         ma.p0_known = 1; ma.p0v = p0;
-        ma.nodes = P.nodes; ma.node_offset = 0;
+        ma.nodes = P.nodes; ma.node_offset = P.node_offset;
         ma.dbg = P.mdbg;
+        ma.low_prio = P.merge_low_prio;
         ma.out_rec = reinterpret_cast<Rec *>(lb);
         ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
+        const bool xchg = P.R > 1 && p0 + m < NP;  // block-uniform
+        if (xchg) ma.lds_msg = s_msg;
         merge_pod_body<KC, K, true>(ma, m);
+        if (xchg) {
+            // this rank's list of pod m -> slot (a % 4, rank, m) of every rank's ring; then the R lists of
+            // pod m from this rank's ring -> rank merge -> the commit's list (lring)
+            constexpr int MW = msg_words(K);
+            const int R = P.R;
+            const uint32_t tag = P.epoch0 + (uint32_t)nact;
+            __syncthreads();
+            for (int e = tid; e < MW * R; e += kMergeThreads) {
+                const int r = e / MW, w = e % MW;
+                uint64_t *dst = reinterpret_cast<uint64_t *>(
+                    P.rx_peer[r] + ((size_t)(slot * R + P.rank) * P.B + m) * (size_t)P.xchg_stride);
+                st_sys(dst + w, (uint64_t)s_msg[w] | ((uint64_t)tag << 32));
+            }
+            bool ok = true;
+            const char *own = P.rx_peer[P.rank];
+            for (int e = tid; e < MW * R; e += kMergeThreads) {
+                const int r = e / MW, w = e % MW;
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(
+                    own + ((size_t)(slot * R + r) * P.B + m) * (size_t)P.xchg_stride);
+                uint32_t word = 0;
+                if (ok && !granule_wait(src + w, tag, P.timeout_ticks, &word)) ok = false;
+                s_all[e] = word;
+            }
+            if (!ok) set_err(P.err, 10);
+            s_stop = 0;
+            __syncthreads();
+            if (!ok) s_stop = 1;
+            __syncthreads();
+            if (s_stop) return;
+            if (tid < 64) rank_merge_msgs<K>(s_all, R, ma.out_rec + (size_t)m * K, ma.out_fc + m);
+        }
         drain_stores();
         __syncthreads();
+        if (tid == 0 && m == 0) st_coh(&ctl->nact, (uint64_t)nact);
         if (tid == 0) {
             const unsigned long long d =
                 __hip_atomic_fetch_add(&ctl->merged[slot], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (d + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
         }
     }
+}
+
+// All ranks meet on the device and agree on the minimum of `mine` (tag: this call's epoch0; the
+// batches of the call use epoch0 + 1, ...).  One wave; lane r < R writes rank r's barrier granule.
+__global__ __launch_bounds__(64) void k_xchg_min(PersistArgs P, int32_t mine, int32_t *out) {
+    const int lane = threadIdx.x;
+    const size_t off = (size_t)4 * P.R * P.B * (size_t)P.xchg_stride;
+    const uint32_t tag = P.epoch0;
+    if (lane < P.R) st_sys(reinterpret_cast<uint64_t *>(P.rx_peer[lane] + off) + P.rank, (uint64_t)(uint32_t)mine | ((uint64_t)tag << 32));
+    int32_t v = 0x7fffffff;
+    bool ok = true;
+    if (lane < P.R) {
+        uint32_t w = 0;
+        ok = granule_wait(reinterpret_cast<const uint64_t *>(P.rx_peer[P.rank] + off) + lane, tag, P.timeout_ticks, &w);
+        v = (int32_t)w;
+    }
+    v = wave_min_i32(v);
+    const bool bad = __ballot(!ok) != 0;
+    if (lane == 0) {
+        if (bad) set_err(P.err, 11);
+        *out = bad ? -1 : v;
+    }
+}
+
+hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hipStream_t s) {
+    if (a.R < 2 || a.R > kMaxXchgRanks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_xchg_min, dim3(1), dim3(64), 0, s, a, mine, out);
+    return hipGetLastError();
 }
 
 size_t persist_score_lds(int KC, int rows_per_wg) {

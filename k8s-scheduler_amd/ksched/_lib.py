@@ -28,6 +28,7 @@ PRIORITY_RESOURCE, PRIORITY_BEST_PRICE = 0, 1
 DOMAIN_ALL, DOMAIN_FEASIBLE = 0, 1
 REASON_FIT, REASON_CPU, REASON_MEMORY, REASON_POD, REASON_LABELS = 0, 1, 2, 3, 4
 NUM_REASONS = 5
+XCHG_HANDLE_BYTES = 64
 # the reference's per-node failure text (anchor/predicate.go:135,140,145)
 REASON_TEXT = {REASON_CPU: "Insufficient CPU", REASON_MEMORY: "Insufficient Memory", REASON_POD: "Insufficient Pod",
                REASON_LABELS: "node labels do not match the pod's selector"}
@@ -80,6 +81,9 @@ SIGNATURES = [
     ("ksched_group_create", C.c_int, [C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("ksched_group_destroy", C.c_int, [C.c_void_p]),
     ("ksched_set_group", C.c_int, [CTX, C.c_void_p]),
+    ("ksched_xchg_export", C.c_int, [CTX, C.c_char_p]),
+    ("ksched_xchg_import", C.c_int, [CTX, C.c_char_p]),
+    ("ksched_xchg_ready", C.c_int, [CTX]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
     ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),
@@ -117,7 +121,7 @@ def lib():
             fn = getattr(lb, name)
             fn.restype = res
             fn.argtypes = args
-        if lb.ksched_abi_version() != 2:
+        if lb.ksched_abi_version() != 3:
             raise ImportError("libksched ABI version mismatch")
         _lib = lb
     return _lib

@@ -5,7 +5,10 @@ index, so the lowest-index tie-break is unchanged).  Every rank scores all pendi
 shard; per speculative batch the ranks exchange their local top-K candidate records (with the
 candidates' snapshot node state) by ONE RCCL all-gather issued inside the engine, merge them
 identically, and replay the same ordered commit -- each rank writes back only the nodes it owns.
-torch.distributed is used only to hand the 128-byte RCCL unique id from rank 0 to the others.
+Two exchange transports: the persistent pipeline's device-side exchange (ksched_xchg_*: merger
+workgroups write every pod's list straight into each rank's receive ring over xGMI, no launch per
+batch), or one RCCL all-gather per batch in the stream pipeline.  torch.distributed only hands out
+the 128-byte RCCL unique id and the 64-byte IPC handles of the rings.
 """
 from __future__ import annotations
 
@@ -37,10 +40,36 @@ def broadcast_bytes(payload, rank: int, src: int = 0) -> bytes:
     return obj[0]
 
 
-def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group=None, **kw):
+def setup_exchange(eng, rank: int, world: int, pg=None) -> bool:
+    """Device-side candidate exchange (ksched_xchg_*): every rank exports its receive ring's IPC handle,
+    the handles are all-gathered over torch.distributed (`pg`, default group), every rank maps them.
+    All ranks agree on the outcome: if any rank fails, none uses the exchange (False)."""
+    import torch.distributed as dist
+    ok, h = 1, b""
+    try:
+        h = eng.xchg_export()
+    except Exception:
+        ok = 0
+    hs = [None] * world
+    dist.all_gather_object(hs, (ok, h), group=pg)
+    ok = int(all(x[0] for x in hs))
+    if ok:
+        try:
+            eng.xchg_import([x[1] for x in hs])
+        except Exception:
+            ok = 0
+    flags = [None] * world
+    dist.all_gather_object(flags, ok, group=pg)
+    return all(flags)
+
+
+def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group=None, comm: bool = True,
+                        xchg: bool = False, pg=None, **kw):
     """Engine for this rank's node shard of cluster `cl`.  world > 1: joined to the other ranks by an
-    RCCL communicator (one process per GPU, torch.distributed hands out the id), or -- `group` given --
-    by an in-process rank group (ranks as threads of this process on one device)."""
+    RCCL communicator (one process per GPU, torch.distributed hands out the id; comm=False skips it), or
+    -- `group` given -- by an in-process rank group (ranks as threads of this process on one device).
+    xchg=True also sets up the device-side exchange of the persistent pipeline (setup_exchange);
+    the returned engine's `xchg_ready` tells whether it took."""
     from . import _lib as L
     from .engine import Engine
     lo, hi = shard_range(cl.n_nodes, rank, world)
@@ -54,9 +83,12 @@ def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group
     if group is not None:
         eng.set_group(group)
     elif world > 1:
-        uid = Engine.unique_id() if rank == 0 else None
-        uid = broadcast_bytes(uid, rank)
-        eng.set_comm(uid)
+        if comm:
+            uid = Engine.unique_id() if rank == 0 else None
+            uid = broadcast_bytes(uid, rank)
+            eng.set_comm(uid)
+        if xchg:
+            setup_exchange(eng, rank, world, pg=pg)
     return eng, (lo, hi)
 
 

@@ -100,6 +100,22 @@ class Engine:
         assert len(uid) == 128
         self._chk(L.lib().ksched_set_comm(self._ctx, uid), "set_comm")
 
+    def xchg_export(self) -> bytes:
+        """Allocate this rank's receive ring of the device-side exchange; returns its IPC handle."""
+        buf = C.create_string_buffer(L.XCHG_HANDLE_BYTES)
+        self._chk(L.lib().ksched_xchg_export(self._ctx, buf), "xchg_export")
+        return buf.raw
+
+    def xchg_import(self, handles):
+        """Map every rank's ring (handles in rank order, as xchg_export returned them)."""
+        blob = b"".join(handles)
+        assert len(blob) == L.XCHG_HANDLE_BYTES * self.opts.nranks
+        self._chk(L.lib().ksched_xchg_import(self._ctx, blob), "xchg_import")
+
+    @property
+    def xchg_ready(self) -> bool:
+        return bool(L.lib().ksched_xchg_ready(self._ctx))
+
     def set_group(self, group: "Group"):
         self._chk(L.lib().ksched_set_group(self._ctx, group._h), "set_group")
         self._group = group  # keep the group alive as long as this context

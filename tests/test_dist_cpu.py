@@ -135,3 +135,60 @@ def test_sharded_equals_sequential(oracle_mod, case):
     for a, b in zip(st, wst):
         assert np.array_equal(a, b)
     assert batches >= 1
+
+
+class _FakeXchgEngine:
+    """Stands in for ksched.Engine in the exchange setup (CPU): export returns a per-rank handle or
+    fails, import records what it was given."""
+
+    def __init__(self, rank, fail_export=False, fail_import=False):
+        self.rank, self.fail_export, self.fail_import = rank, fail_export, fail_import
+        self.imported = None
+
+    def xchg_export(self):
+        if self.fail_export:
+            raise RuntimeError("no IPC")
+        return bytes([self.rank]) * 64
+
+    def xchg_import(self, handles):
+        if self.fail_import:
+            raise RuntimeError("cannot map")
+        self.imported = list(handles)
+
+
+def _xchg_worker(rank, world, port, fail_rank, fail_where, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "k8s-scheduler_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    from ksched.dist import setup_exchange
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = _FakeXchgEngine(rank, fail_export=(rank == fail_rank and fail_where == "export"),
+                              fail_import=(rank == fail_rank and fail_where == "import"))
+        ok = setup_exchange(eng, rank, world)
+        q.put((rank, ok, eng.imported))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,fail_rank,fail_where", [(2, -1, ""), (3, -1, ""), (2, 1, "export"), (3, 0, "import")])
+def test_exchange_setup_agreement(world, fail_rank, fail_where):
+    """ksched.dist.setup_exchange (device-side exchange of the persistent pipeline): the ranks'
+    IPC handles are all-gathered in rank order, and every rank reports the same outcome -- one
+    rank failing to export or map makes ALL ranks fall back together (bench.py relies on it)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xchg_worker, args=(r, world, port, fail_rank, fail_where, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (ok, imp)) for r, ok, imp in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=30)
+    oks = {ok for ok, _ in res.values()}
+    assert oks == {fail_rank < 0}, res
+    if fail_rank < 0:
+        for r in range(world):
+            assert res[r][1] == [bytes([k]) * 64 for k in range(world)]

@@ -1,0 +1,39 @@
+"""Worker of tests/test_gpu_xchg.py: one rank of the node-sharded persistent pipeline with the
+device-side exchange, as its own process (several ranks share the test box's one GPU).  Not a test
+module: spawned by the test with multiprocessing."""
+import os
+import sys
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd")]
+
+
+def run_rank(rank, world, port, cfg, nn, pp, calls, q):
+    try:
+        # ranks on ONE device: each grid takes its share of the CUs (one score workgroup per CU, one
+        # free CU per XCD and rank for the commits), so all ranks' workgroups are resident together
+        os.environ["KSCHED_PERSIST_G"] = str(max(8, (256 - 8 * world) // world // 8 * 8))
+        os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "5000")
+        import numpy as np
+        import torch.distributed as dist
+        from ksched import MODE_BATCHED, cluster
+        from ksched.dist import make_sharded_engine
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
+        eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=0, mode=MODE_BATCHED, comm=False, xchg=True,
+                                            topk=16, batch=64)
+        assert eng.xchg_ready, "exchange setup failed"
+        out = []
+        eng.save_state()
+        for c in range(calls):  # repeated calls: the granule tags advance across calls
+            eng.restore_state()
+            oi, os_, of = eng.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+            st = eng.stats()
+            out.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"]))
+        state = eng.read_nodes()
+        eng.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", out, (lo, hi), state))
+    except Exception:
+        q.put((rank, "error", traceback.format_exc(), None, None))
