@@ -140,7 +140,7 @@ def main():
         # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, each grid on its share of
         # the CUs, torch.distributed over gloo, no RCCL communicator (RCCL refuses two ranks per GPU)
         local = 0
-        os.environ.setdefault("KSCHED_PERSIST_G", str(max(8, (256 - 8 * world) // world // 8 * 8)))
+        os.environ.setdefault("KSCHED_PERSIST_G", str(max(8, (256 - 34 * world) // world // 8 * 8)))
     tdev = "cpu" if args.same_device else "cuda"
     if world > 1:
         import torch

@@ -139,8 +139,15 @@ __device__ __forceinline__ LanePods load_lane_pods(const PodArgs &pods, int64_t 
     return q;
 }
 
-template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH>
-__device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr) {
+struct NoWait {
+    __device__ bool operator()() const { return true; }
+};
+
+// wait(): called by every thread once the work that needs no candidate list is done (the persistent
+// commit waits there for the batch's merges); false = give up (the caller reports the timeout).
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH, typename Wait = NoWait>
+__device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr,
+                                                 Wait wait = Wait{}) {
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -148,6 +155,7 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
     const int64_t p0 = COH ? L->plan[A.batch % kPlanRing] : load_i64<COH>(A.plan);
     const int64_t cursor = COH ? L->cursor : load_i64<COH>(&A.ctl->cursor);
     if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
+        if (!wait()) return false;
         // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
         if (wave == 0) {
             if (lane == 0) {
@@ -164,10 +172,11 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
             }
             publish_committed<COH>(A);
         }
-        return;
+        return true;
     }
     const bool dbg = A.dbg != nullptr;  // diagnostics build of the phase timing (KSCHED_COMMIT_STAMPS)
-    const uint64_t t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t t_pre = 0;
     uint64_t t_s1 = 0, t_s2 = 0, t_s3 = 0, t_mark = 0;
     SpcSmem m;
     {
@@ -199,43 +208,35 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
     const LanePods lp = pre ? *pre : load_lane_pods<LAB>(A.pods, p0, nb);
     const int64_t rc = lp.rc, rm = lp.rm, rp = lp.rp;
     const uint64_t sel = lp.sel;
-    const int64_t fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
-    const int cut0 = (wave == 0 && pj) ? load_rec<COH>(A.lists + (size_t)lane * K).pad : 0;
-
-    // every thread's list entries: only their (key, idx | valid) words, all loads in flight at once,
-    // issued before the table initialisation so their latency overlaps it
+    // the batch's candidate lists: fc0 and cut flag per pod, and every thread's list entries -- only
+    // their (key, idx | valid) words, all loads in flight at once.  Lists that are ready at entry (the
+    // stream pipeline) are loaded before the table initialisation so their latency overlaps it; the
+    // persistent commit loads them after wait(), when the merges have published them.
     constexpr int kHeadPer = (64 * K + kSpcThreads - 1) / kSpcThreads;
     uint64_t w0[kHeadPer], w1[kHeadPer];
-#pragma unroll
-    for (int u = 0; u < kHeadPer; ++u) {
-        const int e = tid + u * kSpcThreads;
-        w0[u] = 0; w1[u] = 0;  // valid = 0
-        if (e < 64 * K && e / K < nb) {
-            const uint64_t *w = reinterpret_cast<const uint64_t *>(A.lists + e);
-            if (COH) { w0[u] = ld_coh(w); w1[u] = ld_coh(w + 1); }
-            else { w0[u] = w[0]; w1[u] = w[1]; }
-        }
-    }
-
-    // ---- prologue (all waves) ----
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
-    if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
-    __syncthreads();
-    {
+    int64_t fc0v = 0;
+    int cut0 = 0;
+    auto load_lists = [&]() {
+        fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
+        cut0 = (wave == 0 && pj) ? (int32_t)(uint32_t)(load_i64<COH>(
+                                       reinterpret_cast<const int64_t *>(A.lists + (size_t)lane * K) + 6) >> 32) : 0;
 #pragma unroll
         for (int u = 0; u < kHeadPer; ++u) {
             const int e = tid + u * kSpcThreads;
-            if (e < 64 * K) {
-                const int j = e / K, q = e % K;
-                const bool v = (uint32_t)(w1[u] >> 32) != 0;
-                const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
-                const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
-                m.LK[q * 64 + j] = key;
-                m.LI[q * 64 + j] = idx;
-                m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
+            w0[u] = 0; w1[u] = 0;  // valid = 0
+            if (e < 64 * K && e / K < nb) {
+                const uint64_t *w = reinterpret_cast<const uint64_t *>(A.lists + e);
+                if (COH) { w0[u] = ld_coh(w); w1[u] = ld_coh(w + 1); }
+                else { w0[u] = w[0]; w1[u] = w[1]; }
             }
         }
-    }
+    };
+    if constexpr (!COH) load_lists();
+
+    // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
+    if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
+    __syncthreads();
     const int nin = COH ? L->xcount : A.xin->count;  // <= 64
     for (int e = tid; e < nin; e += kSpcThreads) {
         const XRec xi = COH ? L->xe[e] : A.xin->e[e];
@@ -272,6 +273,25 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
         m.pbk[wave * 64 + lane] = pk;
         m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
         if (dfl != 0) atomicAdd(&m.dfacc[lane], dfl);
+    }
+
+    // ---- prologue part 2: the candidate lists (hash positions of their entries) ----
+    if (dbg) t_pre = __builtin_amdgcn_s_memtime() - t_start;
+    if (!wait()) return false;  // a workgroup barrier when it waits
+    if (dbg) t_start = __builtin_amdgcn_s_memtime();
+    if constexpr (COH) load_lists();
+#pragma unroll
+    for (int u = 0; u < kHeadPer; ++u) {
+        const int e = tid + u * kSpcThreads;
+        if (e < 64 * K) {
+            const int j = e / K, q = e % K;
+            const bool v = (uint32_t)(w1[u] >> 32) != 0;
+            const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
+            const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
+            m.LK[q * 64 + j] = key;
+            m.LI[q * 64 + j] = idx;
+            m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
+        }
     }
     __syncthreads();
 
@@ -367,9 +387,11 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
                 gg[u] = __builtin_amdgcn_readfirstlane(k < rce ? m.gn[k] : -1);
                 ss[u] = 0; ra0[u] = ra1[u] = ra2[u] = 0; rlab[u] = 0; rpr[u] = 0.f;
                 if (gg[u] >= 0) {
-                    const Rec r = load_rec<COH>(A.lists + (size_t)k * K + __builtin_amdgcn_readfirstlane(m.gq[k]));
+                    int64_t ra[3];
+                    load_rec_state<COH>(A.lists + (size_t)k * K + __builtin_amdgcn_readfirstlane(m.gq[k]), ra, &rlab[u],
+                                        &rpr[u]);
                     ss[u] = __builtin_amdgcn_readfirstlane(m.gs[k]);
-                    ra0[u] = r.a[0]; ra1[u] = r.a[1]; ra2[u] = r.a[2]; rlab[u] = r.labels; rpr[u] = r.price;
+                    ra0[u] = ra[0]; ra1[u] = ra[1]; ra2[u] = ra[2];
                 }
             }
 #pragma unroll
@@ -524,8 +546,9 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
                         uint64_t lab;
                         float pr;
                         if (kf == 1) {  // first touch of list entry qf
-                            const Rec r = load_rec<COH>(A.lists + (size_t)f * K + qf);
-                            b0 = r.a[0]; b1 = r.a[1]; b2 = r.a[2]; lab = r.labels; pr = r.price;
+                            int64_t ra[3];
+                            load_rec_state<COH>(A.lists + (size_t)f * K + qf, ra, &lab, &pr);
+                            b0 = ra[0]; b1 = ra[1]; b2 = ra[2];
                             s = nT++;
                         } else {
                             const SpcSlot &x = m.T[s];
@@ -583,7 +606,7 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
         if (m.ctl[2]) break;
         c = m.ctl[0];
     }
-    if (wave != 0) return;
+    if (wave != 0) return true;
 
     if (lane < done) {
         A.out.idx[p0 + lane] = my_idx;
@@ -632,9 +655,11 @@ __device__ __forceinline__ void commit_spc_batch(const CommitArgs &A, char *smem
             A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1;
             A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
             A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
+            A.dbg[6] += t_pre;
         }
     }
     publish_committed<COH>(A);  // wave 0 made every global store of this batch
+    return true;
 }
 
 // <= 192 VGPRs (amdgpu_num_vgpr counts half the unified gfx950 file): beside a resident score
@@ -684,31 +709,32 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
             return;
         }
         LanePods pre{0, 0, 0, 0};
-        if (p0 >= 0 && p0 < P.pods.p) {
+        const bool act = p0 >= 0 && p0 < P.pods.p;
+        if (act) {
             idle = 0;
             ++nact;
-            // the pods' requests are known now: their loads overlap the wait for the merges
+            // the pods' requests are known now: their loads overlap the inherited-slot work
             if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
-            if (threadIdx.x == 0) {
-                const uint64_t t0 = wall_clock64();
-                s_stop = 0;
-                const int slot = (int)((nact - 1) % 4);
-                const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
-                while (__hip_atomic_load(&ctl->merged[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-                    if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) { s_stop = 1; break; }
-                    __builtin_amdgcn_s_sleep(1);
-                }
-            }
-            __syncthreads();
-            if (s_stop) {
-                if (threadIdx.x == 0) {
-                    atomicCAS(P.err, 0, 5);
-                    __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                return;
-            }
         }
-        if (threadIdx.x == 0) trace_at(P, b, 3);
+        // the batch's merges (everything of the commit that needs no candidate list runs before this)
+        auto wait_merged = [&]() -> bool {
+            if (act) {
+                if (threadIdx.x == 0) {
+                    const uint64_t t0 = wall_clock64();
+                    s_stop = 0;
+                    const int slot = (int)((nact - 1) % 4);
+                    const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
+                    while (__hip_atomic_load(&ctl->merged[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+                        if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) { s_stop = 1; break; }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                __syncthreads();
+                if (s_stop) return false;
+            }
+            if (threadIdx.x == 0) trace_at(P, b, 3);
+            return true;
+        };
         CommitArgs ca{};
         char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
         ca.lists = reinterpret_cast<const Rec *>(lb);
@@ -724,7 +750,13 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
         ca.dbg = P.cdbg;
         ca.loc = &loc;
-        commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem, &pre);
+        if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem, &pre, wait_merged)) {
+            if (threadIdx.x == 0) {
+                atomicCAS(P.err, 0, 5);
+                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return;
+        }
         __syncthreads();
         if (threadIdx.x == 0) trace_at(P, b, 4);
         if (loc.cursor >= P.pods.p) {

@@ -99,6 +99,18 @@ __device__ __forceinline__ Rec load_rec(const Rec *p) {
         return r;
     }
 }
+// The node-state words of a Rec only (a[3], labels, price: words w2..w6) -- what a commit needs of a
+// candidate it already knows by key and index.
+template <bool COH>
+__device__ __forceinline__ void load_rec_state(const Rec *p, int64_t *a, uint64_t *labels, float *price) {
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
+    uint64_t v[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v[i] = COH ? ld_coh(w + 2 + i) : w[2 + i];
+    a[0] = (int64_t)v[0]; a[1] = (int64_t)v[1]; a[2] = (int64_t)v[2];
+    *labels = v[3];
+    *price = __uint_as_float((uint32_t)v[4]);
+}
 template <bool COH>
 __device__ __forceinline__ void store_rec(Rec *p, const Rec &r) {
     if constexpr (!COH) {

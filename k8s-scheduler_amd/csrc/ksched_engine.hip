@@ -541,10 +541,10 @@ void print_persist_trace(ksched_ctx *c) {
     if (c->d_dbg) {
         int64_t hd[16];
         if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14])
-            fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f failures %lld | cycles/batch: prologue %.0f "
-                    "guess %.0f evaluate %.0f check %.0f total %.0f\n", (long long)hd[14], (double)hd[12] / hd[14],
-                    (long long)hd[13], (double)hd[0] / hd[14], (double)hd[1] / hd[14], (double)hd[2] / hd[14],
-                    (double)hd[3] / hd[14], (double)hd[4] / hd[14]);
+            fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f failures %lld | cycles/batch: before the "
+                    "wait %.0f | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n", (long long)hd[14],
+                    (double)hd[12] / hd[14], (long long)hd[13], (double)hd[6] / hd[14], (double)hd[0] / hd[14],
+                    (double)hd[1] / hd[14], (double)hd[2] / hd[14], (double)hd[3] / hd[14], (double)hd[4] / hd[14]);
     }
     if (c->d_mdbg) {
         int64_t hm[8];
@@ -656,6 +656,7 @@ int enqueue_persistent(ksched_ctx *c) {
     const hipError_t e =
         launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC, sM);
     if (e == hipErrorInvalidValue) {  // does not fit after all: the stream pipeline runs
+        if (env_int("KSCHED_DEBUG", 0)) fprintf(stderr, "[ksched persist] launch_persist: does not fit\n");
         c->timed.clear();
         c->ev_used = 0;
         return 1;
@@ -1197,8 +1198,9 @@ int ksched_selftest_fastdiv(ksched_ctx *c, int64_t n, const double *a, const dou
 int ksched_run(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
     if (c->n_local < 0) return fail(c, KSCHED_E_STATE, "run before load_nodes");
-    if (c->o.nranks > 1 && !c->comm && !c->group)
-        return fail(c, KSCHED_E_STATE, "run: multi-rank context without ksched_set_comm / ksched_set_group");
+    if (c->o.nranks > 1 && !c->comm && !c->group && !c->xchg_ready)
+        return fail(c, KSCHED_E_STATE, "run: multi-rank context without ksched_set_comm / ksched_set_group / "
+                                       "ksched_xchg_import");
     HIPCHK(c, hipSetDevice(c->dev));
     c->err.clear();
     c->st = ksched_stats{};
@@ -1275,23 +1277,21 @@ int ksched_sync(ksched_ctx *c) {
         if (e) c->xchg_ready = false;  // the rings' state is unknown: later calls take the RCCL path
         c->xchg_run = false;
     }
-    if (e == 10 || e == 11) {
-        hipMemset(c->d_err, 0, sizeof(int32_t));
-        return fail(c, KSCHED_E_DEVICE, e == 10 ? "node-sharded exchange: a merger's wait for a peer rank's candidate lists timed out"
-                                                : "node-sharded exchange: the device barrier timed out");
-    }
-    if (e >= 5 && e <= 9) {
+    if (e >= 5 && e <= 11) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
         static const char *what[] = {"the commit's wait for the merges", "a score workgroup's wait for commit(b-2)",
                                      "a merger's wait for the score workgroups", "the score grid's plan (idle)",
-                                     "the commit's plan (idle)"};
+                                     "the commit's plan (idle)", "(unused)",
+                                     "a merger's wait for a peer rank's candidate lists (node-sharded exchange)",
+                                     "the ranks' device barrier (node-sharded exchange)"};
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
-        char buf[320];
+        char buf[400];
         snprintf(buf, sizeof buf,
                  "persistent pipeline: %s timed out (committed %llu, arrive %llu/%llu/%llu/%llu, merged "
-                 "%llu/%llu/%llu/%llu, cursor %lld)",
+                 "%llu/%llu/%llu/%llu, cursor %lld, merger-0 batches %lld, rank %d/%d)",
                  what[e - 5], h->committed, h->arrive[0], h->arrive[1], h->arrive[2], h->arrive[3], h->merged[0],
-                 h->merged[1], h->merged[2], h->merged[3], (long long)h->cursor);
+                 h->merged[1], h->merged[2], h->merged[3], (long long)h->cursor, (long long)h->nact, c->o.rank,
+                 c->o.nranks);
         return fail(c, KSCHED_E_DEVICE, buf);
     }
     if (e == 2 || e == 4) {

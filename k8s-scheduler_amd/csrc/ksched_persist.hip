@@ -21,6 +21,9 @@
 // inherits b-1's), so results are bit-identical; tests/test_gpu_parity.py runs both.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "ksched_kernels.h"
 #include "ksched_merge.h"
 
@@ -326,8 +329,10 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
 // The merge side: B workgroups, one per pod slot of a batch, resident beside the score grid (small LDS).
 // Per active batch: wait for the G arrivals, merge pod m's G lists into its K-entry Rec list (sc1),
 // count the merge.  The score workgroups never merge, so a merge never delays the next batch's scan.
+// <= 112 VGPRs (amdgpu_num_vgpr counts half the unified gfx950 file): two merger waves per SIMD
+// beside the score grid's two (up to 144 VGPRs at KC = 8)
 template <int KC, int K>
-__global__ __launch_bounds__(kMergeThreads) void k_persist_merge(PersistArgs P) {
+__global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56))) void k_persist_merge(PersistArgs P) {
     __shared__ int64_t s_p0, s_done;
     __shared__ int s_stop;
     __shared__ uint32_t s_msg[msg_words(K)];                  // this rank's list of pod m (R > 1)
@@ -482,6 +487,9 @@ hipError_t persist_one(const PersistArgs &a, size_t lds, hipStream_t s, hipStrea
     // one score workgroup + one merger workgroup per CU: LDS, and two waves per SIMD of each in the
     // 512-entry VGPR file (granule 8) -- otherwise the caller falls back to the stream pipeline
     auto vg = [](int r) { return (r + 7) / 8 * 8; };
+    if (std::getenv("KSCHED_DEBUG"))
+        fprintf(stderr, "[ksched persist] score: %d VGPRs %zu+%zu B LDS; merger: %d VGPRs %zu B LDS\n", at.numRegs,
+                (size_t)at.sharedSizeBytes, lds, am.numRegs, (size_t)am.sharedSizeBytes);
     if (at.sharedSizeBytes + lds + am.sharedSizeBytes > 160 * 1024) return hipErrorInvalidValue;
     if (2 * vg(at.numRegs) + 2 * vg(am.numRegs) > 512) return hipErrorInvalidValue;
     if (!launch) return hipSuccess;

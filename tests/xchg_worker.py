@@ -11,9 +11,10 @@ sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd")]
 
 def run_rank(rank, world, port, cfg, nn, pp, calls, q):
     try:
-        # ranks on ONE device: each grid takes its share of the CUs (one score workgroup per CU, one
-        # free CU per XCD and rank for the commits), so all ranks' workgroups are resident together
-        os.environ["KSCHED_PERSIST_G"] = str(max(8, (256 - 8 * world) // world // 8 * 8))
+        # ranks on ONE device (test harness only; one GPU per rank in production): each score grid takes
+        # its share of the CUs, leaving enough free CUs that every rank's commit workgroup (exclusive CU)
+        # still finds one after the other ranks' mergers (up to two per free CU) have landed
+        os.environ["KSCHED_PERSIST_G"] = str(max(8, (256 - 34 * world) // world // 8 * 8))
         os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "5000")
         import numpy as np
         import torch.distributed as dist
