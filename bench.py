@@ -199,13 +199,43 @@ def main():
     if persistent:
         eng.set_timing(True, 1)
     step_stats = []
+    fallbacks = []
+
+    def guarded_step():
+        """step(); if the persistent pipeline reports a device timeout (every wait in it is bounded), the
+        same step is redone on the stream pipeline -- inside the timed region, so the lost time counts --
+        and the failure is reported in the JSON line.  Ranks agree on it (N > 1)."""
+        from ksched import KschedError
+        err = None
+        try:
+            r = step()
+        except KschedError as ex:
+            err, r = str(ex), None
+        if dist is not None:
+            t = torch.tensor([0 if err else 1], dtype=torch.int32, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            failed = int(t.item()) == 0
+        else:
+            failed = err is not None
+        if not failed:
+            return r
+        fallbacks.append(err or "a peer rank failed")
+        print(f"rank {rank}: persistent pipeline failed ({err}); redoing the step on the stream pipeline",
+              file=sys.stderr, flush=True)
+        os.environ["KSCHED_PERSIST"] = "0"
+        os.environ["KSCHED_XCHG"] = "0"
+        try:
+            return step()
+        finally:
+            os.environ.pop("KSCHED_PERSIST", None)
+
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
-        if persistent:
+        res = guarded_step()
+        if persistent and not fallbacks:
             step_stats.append(eng.stats())
     torch.cuda.synchronize()
     if dist is not None:
@@ -255,6 +285,22 @@ def main():
     }
     if pmc:
         roof.update({k: v for k, v in pmc.items() if k != "traffic"})
+    if persistent and mode == MODE_BATCHED:
+        # What actually binds: the 24 B/pair HBM figure above is SURVEY 8d's
+        # bookkeeping -- node rows live in LDS for the whole call, so the score scan moves ~no HBM bytes.
+        # The scan is FP64-VALU work (ISA of the c4 loop: 40 FP64 + 70 other VALU wave-instructions per row of
+        # 64 pairs; FP64 at 4 cycles, other VALU at 2 cycles per wave64 instruction on a 16-lane SIMD), and
+        # the call is bound by the lag-2 dependency chain score -> merge -> commit -> score(b+2).
+        cyc_per_pair = (40 * 4 + 70 * 2) / 64.0
+        simds, clk = 256 * 4, 2.4e9
+        roof["bound_note"] = "bookkeeping: SURVEY 8d's 24 B/pair node re-read; the rows are LDS-resident"
+        roof["limiter"] = {
+            "what": "lag-2 dependency chain (score -> merge -> commit -> next score); score scan FP64-VALU",
+            "scan_valu_cycles_per_pair": cyc_per_pair,
+            "valu_busy_frac_chip": value / max(world, 1) * cyc_per_pair / (simds * clk),
+            "fp64_tflops_algorithmic": value / max(world, 1) * FLOPS_PER_PAIR / 1e12,
+            "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
+        }
     out = {
         "metric": "pod-node evaluations/sec",
         "value": value,
@@ -283,6 +329,8 @@ def main():
         "kernel_avg_ms": fam_share,
         "roofline": roof,
     }
+    if fallbacks:
+        out["persistent_failures"] = fallbacks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base, mt = cpu_baseline(cl, args.cpu_baseline_s)
         out["cpu_baseline"] = base

@@ -688,10 +688,10 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
     __shared__ PersistLocal loc;
     Ctl *ctl = P.ctl;
     // k_ctl_init ran before this kernel on the stream: take the initial plans / cursor / stats once
-    if (threadIdx.x < kPlanRing) loc.plan[threadIdx.x] = (int64_t)ld_coh(&ctl->plan[threadIdx.x]);
+    if (threadIdx.x < kPlanRing) loc.plan[threadIdx.x] = (int64_t)ld_rmw(&ctl->plan[threadIdx.x]);
     if (threadIdx.x == 0) {
-        loc.cursor = (int64_t)ld_coh(&ctl->cursor);
-        for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_coh(&ctl->stats[i]);
+        loc.cursor = (int64_t)ld_rmw(&ctl->cursor);
+        for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_rmw(&ctl->stats[i]);
         loc.xcount = 0;
     }
     __syncthreads();
@@ -720,14 +720,12 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         auto wait_merged = [&]() -> bool {
             if (act) {
                 if (threadIdx.x == 0) {
-                    const uint64_t t0 = wall_clock64();
-                    s_stop = 0;
                     const int slot = (int)((nact - 1) % 4);
                     const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
-                    while (__hip_atomic_load(&ctl->merged[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-                        if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) { s_stop = 1; break; }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
+                    unsigned long long seen = 0;
+                    prog_at(P, P.G + P.B, b, kProgWaitMerged, 0);
+                    s_stop = poll_ge(&ctl->merged[slot], want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
+                    if (s_stop) prog_at(P, P.G + P.B, b, kProgWaitMerged | kProgTimedOut, seen);
                 }
                 __syncthreads();
                 if (s_stop) return false;
@@ -758,7 +756,10 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
             return;
         }
         __syncthreads();
-        if (threadIdx.x == 0) trace_at(P, b, 4);
+        if (threadIdx.x == 0) {
+            trace_at(P, b, 4);
+            prog_at(P, P.G + P.B, b, kProgCommitted, 0);
+        }
         if (loc.cursor >= P.pods.p) {
             if (threadIdx.x == 0)
                 __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -118,6 +118,8 @@ struct ksched_ctx {
     size_t xbuf_bytes = 0;
     // persistent single-rank pipeline (ksched_persist.hip)
     void *d_pws = nullptr;       // per-workgroup part lists + counts
+    uint64_t *d_prog = nullptr;   // persistent pipeline: per-workgroup progress words (in d_pws)
+    int prog_G = 0, prog_B = 0;
     uint64_t *d_trace = nullptr;  // KSCHED_PERSIST_TRACE: per-batch wall-clock stamps
     int64_t trace_cap = 0;
     size_t pws_bytes = 0;
@@ -592,10 +594,15 @@ int enqueue_persistent(ksched_ctx *c) {
     const size_t cnt_b = align_up((size_t)2 * B * G * sizeof(int64_t), 256);
     const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
     const size_t xb = align_up(xbuf_bytes(B), 256);
-    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb;
+    const size_t prog_b = align_up((size_t)(G + B + 1) * kProgWords * 8, 256);
+    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b;
     if (c->pws_bytes < need) {
-        if (c->d_pws) hipFree(c->d_pws); hipFree(c->d_trace);
+        if (c->d_pws) hipFree(c->d_pws);
+        if (c->d_trace) hipFree(c->d_trace);
+        c->d_trace = nullptr;
+        c->trace_cap = 0;
         c->d_pws = nullptr;
+        c->d_prog = nullptr;
         c->pws_bytes = 0;
         HIPCHK(c, hipMalloc(&c->d_pws, need));
         c->pws_bytes = need;
@@ -612,6 +619,10 @@ int enqueue_persistent(ksched_ctx *c) {
     a.lists_bytes = (int64_t)lists_b;
     a.xring = a.lring + 4 * lists_b;
     a.xbuf_bytes = (int64_t)xb;
+    a.prog = reinterpret_cast<uint64_t *>(a.xring + 5 * xb);
+    c->d_prog = a.prog;
+    c->prog_G = G;
+    c->prog_B = B;
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     fill_xchg_args(c, &a);
     a.merge_low_prio = env_int("KSCHED_MERGE_LOW_PRIO", 0);
@@ -646,6 +657,7 @@ int enqueue_persistent(ksched_ctx *c) {
     hipStream_t sS = c->stream, sC = c->stream2, sM = c->stream3;
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
+    HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + 1) * kProgWords * 8, sS));
     HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit and merge streams start after the initialisation
     HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
     HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
@@ -1241,6 +1253,85 @@ int ksched_run(ksched_ctx *c) {
     return r;
 }
 
+// KSCHED_PERSIST_TRACE: per score workgroup the summed scan time and poll-end -> arrival time, slowest first,
+// with where it ran and whether a merger workgroup shared its CU (PersistArgs::prog words 2, 3).
+static void print_wg_busy(ksched_ctx *c) {
+    if (!c->d_prog) return;
+    const int G = c->prog_G, B = c->prog_B, n = G + B + 1;
+    std::vector<uint64_t> w((size_t)kProgWords * n);
+    if (hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    auto where = [&](int i) { return (uint32_t)(w[kProgWords * i + 1] >> 32); };
+    std::vector<int> order(G);
+    for (int g = 0; g < G; ++g) order[g] = g;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return w[kProgWords * a + 3] > w[kProgWords * b + 3]; });
+    auto shares = [&](int g) {
+        int k = 0;
+        for (int m = 0; m < B; ++m) k += where(G + m) == where(g);
+        return k;
+    };
+    double sum_busy = 0, sum_scan = 0, sum_busy_m = 0, sum_busy_nm = 0;
+    int nm = 0;
+    for (int g = 0; g < G; ++g) {
+        sum_busy += (double)w[kProgWords * g + 3];
+        sum_scan += (double)w[kProgWords * g + 2];
+        if (shares(g)) { sum_busy_m += (double)w[kProgWords * g + 3]; ++nm; } else sum_busy_nm += (double)w[kProgWords * g + 3];
+    }
+    fprintf(stderr, "persist wg busy (ms, 100 MHz ticks): mean scan %.2f busy %.2f | with a merger on the CU (%d WGs) %.2f, "
+                    "without %.2f | slowest:",
+            sum_scan / G * 1e-5, sum_busy / G * 1e-5, nm, nm ? sum_busy_m / nm * 1e-5 : 0.0,
+            G > nm ? sum_busy_nm / (G - nm) * 1e-5 : 0.0);
+    for (int k = 0; k < 8 && k < G; ++k) {
+        const int g = order[k];
+        fprintf(stderr, " #%d(scan %.2f busy %.2f xcc %u se %u cu %u mergers %d)", g, w[kProgWords * g + 2] * 1e-5,
+                w[kProgWords * g + 3] * 1e-5, (where(g) >> 8) & 0xf, (where(g) >> 4) & 0xf, where(g) & 0xf, shares(g));
+    }
+    fprintf(stderr, " | fastest: #%d(busy %.2f)\n", order[G - 1], w[kProgWords * order[G - 1] + 3] * 1e-5);
+}
+
+// After a persistent wait timed out: which workgroups are furthest behind, in which phase, on which XCD/SE/CU,
+// and what their last wait saw (PersistArgs::prog).
+static std::string progress_summary(ksched_ctx *c) {
+    if (!c->d_prog) return "";
+    const int n = c->prog_G + c->prog_B + 1;
+    std::vector<uint64_t> w((size_t)kProgWords * n);
+    if (hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return "";
+    const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
+    std::string out = "; polls satisfied by the atomic read " + std::to_string(h->polls_rmw);
+    auto group = [&](const char *name, int lo, int hi) {
+        int64_t bmin = INT64_MAX, bmax = -1;
+        for (int i = lo; i < hi; ++i) {
+            const int64_t b = (int64_t)(w[kProgWords * i] >> 8);
+            bmin = std::min(bmin, b); bmax = std::max(bmax, b);
+        }
+        char t[160];
+        snprintf(t, sizeof t, "; %s batches %lld..%lld", name, (long long)bmin, (long long)bmax);
+        out += t;
+        int shown = 0;
+        for (int i = lo; i < hi && shown < 6; ++i) {
+            if ((int64_t)(w[kProgWords * i] >> 8) != bmin || bmin == bmax) continue;
+            const uint32_t where = (uint32_t)(w[kProgWords * i + 1] >> 32);
+            snprintf(t, sizeof t, " [#%d phase %#x xcc %u se %u cu %u saw %llu polls %llu]", i - lo,
+                     (unsigned)(w[kProgWords * i] & 0xff), (where >> 8) & 0xf, (where >> 4) & 0xf, where & 0xf,
+                     (unsigned long long)(w[kProgWords * i + 1] & 0xffffffffull),
+                     (unsigned long long)w[kProgWords * i + 2]);
+            out += t;
+            ++shown;
+        }
+    };
+    group("score", 0, c->prog_G);
+    group("merge", c->prog_G, c->prog_G + c->prog_B);
+    group("commit", c->prog_G + c->prog_B, n);
+    {
+        const int i = n - 1;
+        const uint32_t where = (uint32_t)(w[kProgWords * i + 1] >> 32);
+        char t[120];
+        snprintf(t, sizeof t, "; commit phase %#x on xcc %u se %u cu %u", (unsigned)(w[kProgWords * i] & 0xff),
+                 (where >> 8) & 0xf, (where >> 4) & 0xf, where & 0xf);
+        out += t;
+    }
+    return out;
+}
+
 int ksched_sync(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
     HIPCHK(c, hipSetDevice(c->dev));
@@ -1259,7 +1350,10 @@ int ksched_sync(ksched_ctx *c) {
         }
         c->timed.clear();
     }
-    if (c->persist_stats && c->d_trace && env_int("KSCHED_PERSIST_TRACE", 0)) print_persist_trace(c);
+    if (c->persist_stats && c->d_trace && env_int("KSCHED_PERSIST_TRACE", 0)) {
+        print_persist_trace(c);
+        print_wg_busy(c);
+    }
     if (c->persist_stats) {
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
         c->st.batches = h->stats[0];
@@ -1292,7 +1386,7 @@ int ksched_sync(ksched_ctx *c) {
                  what[e - 5], h->committed, h->arrive[0], h->arrive[1], h->arrive[2], h->arrive[3], h->merged[0],
                  h->merged[1], h->merged[2], h->merged[3], (long long)h->cursor, (long long)h->nact, c->o.rank,
                  c->o.nranks);
-        return fail(c, KSCHED_E_DEVICE, buf);
+        return fail(c, KSCHED_E_DEVICE, std::string(buf) + progress_summary(c));
     }
     if (e == 2 || e == 4) {
         hipMemset(c->d_err, 0, sizeof(int32_t));

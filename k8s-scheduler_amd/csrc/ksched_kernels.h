@@ -103,6 +103,7 @@ struct alignas(8) Ctl {
     unsigned long long merged[4];  // merger workgroups done with active batch a: B per use of the slot
     int64_t cursor_at[kPlanRing];  // cursor right after commit(b), slot b % kPlanRing
     int64_t nact;                  // persistent pipeline: active batches of the call (merger 0)
+    unsigned long long polls_rmw;  // persistent waits that only the periodic atomic read satisfied
 };
 
 struct PodArgs {
@@ -356,7 +357,72 @@ struct PersistArgs {
     int64_t xchg_stride;    // bytes per pod message in a ring
     char *rx_peer[8];       // every rank's receive ring, mapped into this process (rx_peer[rank] = own)
     int32_t merge_low_prio; // KSCHED_MERGE_LOW_PRIO: mergers yield issue slots to the score waves
+    // progress words, kProgWords per workgroup ([G] score, [B] merger, [1] commit): {batch << 8 | phase, hw id
+    // << 32 | low word of the last value a wait saw, busy-time sums}; read by the host when a wait timed out
+    // (and by the phase trace)
+    uint64_t *prog;
 };
+// progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
+constexpr int kProgWords = 4;
+enum : int { kProgWaitCommit = 1, kProgScan = 2, kProgArrived = 3, kProgWaitArrive = 4, kProgMerged = 5,
+             kProgWaitMerged = 6, kProgCommitted = 7, kProgIdle = 8, kProgTimedOut = 0x80 };
+__device__ __forceinline__ uint32_t hw_where() {
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    // xcc[3:0] | se[15:13] | cu[11:8] of HW_ID
+    return (xcc & 0xf) << 8 | ((hw >> 13) & 7) << 4 | ((hw >> 8) & 0xf);
+}
+__device__ __forceinline__ void prog_at(const PersistArgs &P, int slot, int64_t b, int phase, uint64_t seen) {
+    if (!P.prog) return;
+    __hip_atomic_store(P.prog + kProgWords * slot, (uint64_t)b << 8 | (uint64_t)phase, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(P.prog + kProgWords * slot + 1, (uint64_t)hw_where() << 32 | (seen & 0xffffffffull),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// busy-time sums of a workgroup (KSCHED_PERSIST_TRACE calls only: P.trace set): word 2 += scan ticks, word 3
+// += ticks from its wait's end to its arrival (word 2 is the heartbeat of a long wait otherwise)
+__device__ __forceinline__ void prog_add(const PersistArgs &P, int slot, uint64_t scan, uint64_t busy) {
+    if (!P.prog || !P.trace) return;
+    P.prog[kProgWords * slot + 2] += scan;
+    P.prog[kProgWords * slot + 3] += busy;
+}
+// Atomic read of a control word at the coherence point: an RMW that adds a zero the compiler cannot see
+// (an idempotent RMW it would turn back into a plain atomic load, which may be served by a cached line).
+__device__ __forceinline__ uint64_t ld_rmw(const void *p) {
+    uint64_t zero = 0;
+    asm volatile("" : "+v"(zero));
+    return __hip_atomic_fetch_add(reinterpret_cast<uint64_t *>(const_cast<void *>(p)), zero, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+}
+// Bounded wait for *p >= v (one lane).  Polls are relaxed agent-scope (sc1) loads with s_sleep; every 1024th
+// poll reads the counter with an atomic RMW instead (performed at the coherence point, never served from a
+// cached line), so a poll can not stay behind the counter for longer than ~1024 sleeps; each such read
+// also stores the poll count to *heartbeat (a stuck wait shows whether it still runs).  A wait that only the
+// RMW read satisfied is counted in *rmw_hits.  false: timed out (*seen = the last value read).
+__device__ __forceinline__ bool poll_ge(const unsigned long long *p, unsigned long long v, int64_t limit,
+                                        unsigned long long *rmw_hits, unsigned long long *seen,
+                                        uint64_t *heartbeat = nullptr) {
+    unsigned long long x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (x >= v) { *seen = x; return true; }
+    const uint64_t t0 = wall_clock64();
+    for (int it = 1;; ++it) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((it & 1023) == 0) {
+            if (heartbeat) __hip_atomic_store(heartbeat, (uint64_t)it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            x = (unsigned long long)ld_rmw(p);
+            if (x >= v) {
+                if (rmw_hits) __hip_atomic_fetch_add(rmw_hits, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *seen = x;
+                return true;
+            }
+            if ((int64_t)(wall_clock64() - t0) > limit) { *seen = x; return false; }
+        } else {
+            x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (x >= v) { *seen = x; return true; }
+        }
+    }
+}
 constexpr int kMaxXchgRanks = 8;
 // receive ring: [4 active-batch slots][R source ranks][B pods] messages, then R barrier granules
 constexpr size_t xchg_stride_bytes(int K) { return ((size_t)msg_words(K) * 8 + 63) / 64 * 64; }

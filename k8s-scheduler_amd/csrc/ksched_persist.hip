@@ -39,13 +39,9 @@ constexpr int kPThreads = kPW * 64;
 constexpr int kPU = KSCHED_PERSIST_PU;     // rows per score step (independent key chains)        // == kMergeThreads: a merger runs merge_pod_body as is
 constexpr size_t kExclusiveLds = 81 * 1024;  // > 160 KiB / 2: one score workgroup per CU
 
-__device__ __forceinline__ bool spin_ge(const unsigned long long *p, unsigned long long v, int64_t limit) {
-    const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < v) {
-        if ((int64_t)(wall_clock64() - t0) > limit) return false;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
+__device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const unsigned long long *p,
+                                        unsigned long long v, unsigned long long *seen) {
+    return poll_ge(p, v, P.timeout_ticks, &P.ctl->polls_rmw, seen, P.prog ? P.prog + kProgWords * slot + 2 : nullptr);
 }
 
 // the first failure names the wait that timed out (ksched_sync reports it)
@@ -150,7 +146,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
     int32_t *s_idx = reinterpret_cast<int32_t *>(fold + (size_t)(kPW / 2) * KC * 64 * 8);
     int32_t *s_cnt = s_idx + (size_t)(kPW / 2) * KC * 64;                 // [64]
     __shared__ int64_t s_p0, s_done;
-    __shared__ int s_stop;
+    __shared__ int s_stop, s_nx;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -172,8 +168,11 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
         // ---- wait for commit(b-2): its plan for b, its exported commits, the cursor after it ----
         if (tid == 0) {
             int stop = 0;
-            if (b >= 2 && !spin_ge(&ctl->committed, (unsigned long long)(b - 1), P.timeout_ticks)) {
+            unsigned long long seen = 0;
+            prog_at(P, g, b, kProgWaitCommit, 0);
+            if (b >= 2 && !spin_ge(P, g, &ctl->committed, (unsigned long long)(b - 1), &seen)) {
                 set_err(P.err, 6);
+                prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
                 stop = 2;
             }
             if (g == 0) trace_at(P, b, 6);
@@ -189,7 +188,9 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
         // ---- apply commit(b-2)'s exported nodes to the rows this workgroup owns ----
         if (b >= 2) {
             const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b - 2) % 4) * P.xbuf_bytes);
-            const int nx = (int)(uint32_t)ld_coh(&xb->count);
+            if (tid == 0) s_nx = (int)(uint32_t)ld_coh(&xb->count);
+            __syncthreads();
+            const int nx = s_nx;
             for (int e = tid; e < nx; e += kPThreads) {
                 const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
                 const int64_t j = (int64_t)(int32_t)(uint32_t)ld_coh(w) - P.node_offset;  // local row
@@ -205,16 +206,22 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
         __syncthreads();
         if (s_done >= NP) break;                  // every pod resolved by commit(b-2) or earlier
         if (p0 < 0 || p0 >= NP) {                 // nothing planned for batch b (identical on every WG)
+            if (tid == 0) prog_at(P, g, b, kProgIdle, (uint64_t)p0);
             // a truncation re-plans within two batches; a longer run of empty plans is a protocol error
             if (++idle > kPlanRing) {
                 if (tid == 0) set_err(P.err, 8);
                 return;
             }
+            __syncthreads();  // every wave has read s_done before thread 0 rewrites it
             continue;
         }
         idle = 0;
         ++nact;
-        if (g == 0 && tid == 0) trace_at(P, b, 0);
+        if (tid == 0) {
+            if (g == 0) trace_at(P, b, 0);
+            prog_at(P, g, b, kProgScan, 0);
+        }
+        const uint64_t t_go = (P.trace && tid == 0) ? wall_clock64() : 0;
         // ---- score: lane = pod, wave w scans rows r = w, w + W, ... (nodes j = g + r G) ----
         if (tid < 64) s_cnt[tid] = 0;
         const int64_t pod = p0 + lane;
@@ -267,6 +274,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
             }
         }
         if (g == 0 && tid == 0) trace_at(P, b, 8);
+        const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
         __syncthreads();  // s_cnt zeroed before any wave adds
         if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
@@ -315,6 +323,8 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
                                                                   __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long use = (unsigned long long)((nact - 1) / 4);
             if (old + 1 == (use + 1) * (unsigned long long)G) trace_at(P, b, 1);
+            prog_at(P, g, b, kProgArrived, old + 1);
+            if (P.trace) prog_add(P, g, t_scan - t_go, wall_clock64() - t_go);
         }
     }
     // every pod is resolved: this workgroup's rows go back to HBM whole (allocatable, cached doubles,
@@ -347,8 +357,11 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
     for (int64_t b = 0;; ++b) {
         if (tid == 0) {
             int stop = 0;
-            if (b >= 2 && !spin_ge(&ctl->committed, (unsigned long long)(b - 1), P.timeout_ticks)) {
+            unsigned long long seen = 0;
+            prog_at(P, P.G + m, b, kProgWaitCommit, 0);
+            if (b >= 2 && !spin_ge(P, P.G + m, &ctl->committed, (unsigned long long)(b - 1), &seen)) {
                 set_err(P.err, 6);
+                prog_at(P, P.G + m, b, kProgWaitCommit | kProgTimedOut, seen);
                 stop = 2;
             }
             s_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
@@ -361,6 +374,7 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
         const int64_t p0 = s_p0;
         if (s_done >= NP) return;
         if (p0 < 0 || p0 >= NP) {
+            if (tid == 0) prog_at(P, G + m, b, kProgIdle, (uint64_t)p0);
             if (++idle > kPlanRing) {
                 if (tid == 0) set_err(P.err, 8);
                 return;
@@ -373,8 +387,13 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
         const int slot = (int)((nact - 1) % 4);
         const unsigned long long use = (unsigned long long)((nact - 1) / 4);
         if (tid == 0) {
-            s_stop = spin_ge(&ctl->arrive[slot], (use + 1) * (unsigned long long)G, P.timeout_ticks) ? 0 : 1;
-            if (s_stop) set_err(P.err, 7);
+            unsigned long long seen = 0;
+            prog_at(P, G + m, b, kProgWaitArrive, 0);
+            s_stop = spin_ge(P, G + m, &ctl->arrive[slot], (use + 1) * (unsigned long long)G, &seen) ? 0 : 1;
+            if (s_stop) {
+                set_err(P.err, 7);
+                prog_at(P, G + m, b, kProgWaitArrive | kProgTimedOut, seen);
+            }
             if (m == 0) trace_at(P, b, 7);
         }
         __syncthreads();
@@ -433,6 +452,7 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
             const unsigned long long d =
                 __hip_atomic_fetch_add(&ctl->merged[slot], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (d + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
+            prog_at(P, G + m, b, kProgMerged, d + 1);
         }
     }
 }
