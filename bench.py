@@ -173,31 +173,6 @@ def main():
         eng.sync()
         return eng.results()
 
-    for w in range(max(args.warmup, 1 if world > 1 else 0)):
-        if world > 1 and w == 0:
-            # every rank must take the same transport: if the exchange failed anywhere (a device
-            # timeout), all ranks fall back to the RCCL stream pipeline together
-            from ksched import KschedError
-            ok = 1
-            try:
-                step()
-            except KschedError as ex:
-                ok = 0
-                print(f"rank {rank}: device-side exchange failed ({ex}); falling back to RCCL", file=sys.stderr)
-            t = torch.tensor([ok], dtype=torch.int32, device=tdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            if int(t.item()) == 0:
-                os.environ["KSCHED_XCHG"] = "0"
-                step()
-        else:
-            step()
-    pipeline = eng.stats()["pipeline"]
-    persistent = pipeline == "persistent"
-    # the persistent pipeline is ONE score-grid launch per step: its HIP events (on the grid's own
-    # stream) cost nothing per batch, so the roofline's launch durations come from the timed steps
-    # themselves.  The stream pipeline samples per-batch events in one extra untimed pass instead.
-    if persistent:
-        eng.set_timing(True, 1)
     step_stats = []
     fallbacks = []
 
@@ -229,13 +204,39 @@ def main():
         finally:
             os.environ.pop("KSCHED_PERSIST", None)
 
+    for w in range(max(args.warmup, 1 if world > 1 else 0)):
+        if world > 1 and w == 0:
+            # every rank must take the same transport: if the exchange failed anywhere (a device
+            # timeout), all ranks fall back to the RCCL stream pipeline together
+            from ksched import KschedError
+            ok = 1
+            try:
+                step()
+            except KschedError as ex:
+                ok = 0
+                print(f"rank {rank}: device-side exchange failed ({ex}); falling back to RCCL", file=sys.stderr)
+            t = torch.tensor([ok], dtype=torch.int32, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if int(t.item()) == 0:
+                os.environ["KSCHED_XCHG"] = "0"
+                step()
+        else:
+            guarded_step()
+    pipeline = eng.stats()["pipeline"]
+    persistent = pipeline == "persistent"
+    # the persistent pipeline is ONE score-grid launch per step: its HIP events (on the grid's own
+    # stream) cost nothing per batch, so the roofline's launch durations come from the timed steps
+    # themselves.  The stream pipeline samples per-batch events in one extra untimed pass instead.
+    if persistent:
+        eng.set_timing(True, 1)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        nf = len(fallbacks)
         res = guarded_step()
-        if persistent and not fallbacks:
+        if persistent and len(fallbacks) == nf:
             step_stats.append(eng.stats())
     torch.cuda.synchronize()
     if dist is not None:
@@ -249,12 +250,12 @@ def main():
     pairs = cl.n_pods * cl.n_nodes
     value = pairs * args.steps / elapsed
     st = step_stats[-1] if step_stats else eng.stats()
-    if persistent:
+    if persistent and step_stats:
         eng.set_timing(False)
         kstats = step_stats
     else:
         eng.set_timing(True, 8)
-        step()
+        guarded_step()
         kstats = [eng.stats()]
         eng.set_timing(False)
     names = (["k_exact"] if mode == MODE_EXACT else ["k_persist_score" if persistent else "k_score_topk"]) + \

@@ -702,10 +702,8 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
             // pods remain but nothing is planned: a truncation re-plans within two batches, so this is a
             // protocol error -- stop everyone instead of spinning
-            if (threadIdx.x == 0) {
-                atomicCAS(P.err, 0, 9);
-                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (threadIdx.x == 0) atomicCAS(P.err, 0, 9);
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
             return;
         }
         LanePods pre{0, 0, 0, 0};
@@ -724,7 +722,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
                     const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
                     unsigned long long seen = 0;
                     prog_at(P, P.G + P.B, b, kProgWaitMerged, 0);
-                    s_stop = poll_ge(&ctl->merged[slot], want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
+                    s_stop = poll_ge(&ctl->merged[slot].v, want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
                     if (s_stop) prog_at(P, P.G + P.B, b, kProgWaitMerged | kProgTimedOut, seen);
                 }
                 __syncthreads();
@@ -749,10 +747,8 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         ca.dbg = P.cdbg;
         ca.loc = &loc;
         if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem, &pre, wait_merged)) {
-            if (threadIdx.x == 0) {
-                atomicCAS(P.err, 0, 5);
-                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (threadIdx.x == 0) atomicCAS(P.err, 0, 5);
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
             return;
         }
         __syncthreads();
@@ -761,8 +757,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
             prog_at(P, P.G + P.B, b, kProgCommitted, 0);
         }
         if (loc.cursor >= P.pods.p) {
-            if (threadIdx.x == 0)
-                __hip_atomic_store(&ctl->committed, 1ull << 62, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
             return;
         }
     }

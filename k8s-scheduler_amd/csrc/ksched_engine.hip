@@ -277,7 +277,7 @@ int decide_fast53(ksched_ctx *c) {
         PersistArgs a{};
         fill_xchg_args(c, &a);
         a.err = c->d_err;
-        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
+        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 2000) * 100000;
         int32_t mn = -1;
         HIPCHK(c, launch_xchg_min(a, flag, c->d_xmin, c->stream));
         HIPCHK(c, hipMemcpyAsync(&mn, c->d_xmin, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -626,10 +626,11 @@ int enqueue_persistent(ksched_ctx *c) {
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     fill_xchg_args(c, &a);
     a.merge_low_prio = env_int("KSCHED_MERGE_LOW_PRIO", 0);
+    a.prog_waves = env_int("KSCHED_PROG_WAVES", 0);
     a.err = c->d_err;
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)
-    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
+    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 2000) * 100000;
     if (env_int("KSCHED_PERSIST_TRACE", 0)) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {
@@ -1315,6 +1316,14 @@ static std::string progress_summary(ksched_ctx *c) {
                      (unsigned long long)(w[kProgWords * i + 1] & 0xffffffffull),
                      (unsigned long long)w[kProgWords * i + 2]);
             out += t;
+            if (i < c->prog_G && w[kProgWords * i + 4]) {
+                out += " waves";
+                for (int v = 0; v < 8; ++v) {
+                    const uint64_t x = w[kProgWords * i + 4 + v];
+                    snprintf(t, sizeof t, " %lld:%#x", (long long)(x >> 8), (unsigned)(x & 0xff));
+                    out += t;
+                }
+            }
             ++shown;
         }
     };
@@ -1383,8 +1392,8 @@ int ksched_sync(ksched_ctx *c) {
         snprintf(buf, sizeof buf,
                  "persistent pipeline: %s timed out (committed %llu, arrive %llu/%llu/%llu/%llu, merged "
                  "%llu/%llu/%llu/%llu, cursor %lld, merger-0 batches %lld, rank %d/%d)",
-                 what[e - 5], h->committed, h->arrive[0], h->arrive[1], h->arrive[2], h->arrive[3], h->merged[0],
-                 h->merged[1], h->merged[2], h->merged[3], (long long)h->cursor, (long long)h->nact, c->o.rank,
+                 what[e - 5], h->committed, h->arrive[0].v, h->arrive[1].v, h->arrive[2].v, h->arrive[3].v, h->merged[0].v,
+                 h->merged[1].v, h->merged[2].v, h->merged[3].v, (long long)h->cursor, (long long)h->nact, c->o.rank,
                  c->o.nranks);
         return fail(c, KSCHED_E_DEVICE, std::string(buf) + progress_summary(c));
     }

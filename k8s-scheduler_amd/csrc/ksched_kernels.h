@@ -87,7 +87,12 @@ struct alignas(8) XBuf {
 // Device-side pipeline control (one per context).  plan[] holds each in-flight batch's first pod
 // (ring of kPlanRing; -1 = nothing to do).  cursor/resync are written by k_commit, spec_next by k_plan.
 constexpr int kPlanRing = 8;
-struct alignas(8) Ctl {
+constexpr int kCtlReplicas = 8;
+struct alignas(128) CtlLine {
+    unsigned long long v;
+    unsigned long long pad[15];
+};
+struct alignas(128) Ctl {
     int64_t cursor;     // first unresolved pod
     int64_t spec_next;  // next speculative batch start
     int64_t resync;     // 1: a batch truncated; the next plan restarts at cursor
@@ -95,15 +100,18 @@ struct alignas(8) Ctl {
     int64_t plan[kPlanRing];
     unsigned long long scored;     // score workgroups finished this call (device hand-off to the merge)
     unsigned long long committed;  // batches committed this call: commit(b) publishes b + 1 (release)
-    // persistent pipeline (ksched_persist.hip)
-    // per active batch a (counted identically by every workgroup), slot a % 4 -- a workgroup can run one
-    // batch ahead of the slowest, so one shared counter would mix batches; four slots cannot (batch
-    // a + 4 waits for commit(a + 2), which waited for every merge of a + 2)
-    unsigned long long arrive[4];  // score workgroups done with active batch a: G per use of the slot
-    unsigned long long merged[4];  // merger workgroups done with active batch a: B per use of the slot
     int64_t cursor_at[kPlanRing];  // cursor right after commit(b), slot b % kPlanRing
     int64_t nact;                  // persistent pipeline: active batches of the call (merger 0)
     unsigned long long polls_rmw;  // persistent waits that only the periodic atomic read satisfied
+    // persistent pipeline (ksched_persist.hip).  Every polled or atomically counted word has a 128-byte line
+    // of its own: one line shared by the commit's flag, 248 pollers and two families of atomic counters
+    // starved single workgroups of their poll loads for seconds on MI355X.
+    // per active batch a (counted identically by every workgroup), slot a % 4 -- a workgroup can run one
+    // batch ahead of the slowest, so one shared counter would mix batches; four slots cannot (batch
+    // a + 4 waits for commit(a + 2), which waited for every merge of a + 2)
+    CtlLine arrive[4];             // score workgroups done with active batch a: G per use of the slot
+    CtlLine merged[4];             // merger workgroups done with active batch a: B per use of the slot
+    CtlLine committed_x[kCtlReplicas];  // Ctl::committed, one replica per XCD: workgroup w polls w % 8
 };
 
 struct PodArgs {
@@ -230,6 +238,16 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
         __hip_atomic_store(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
+    // persistent pipeline: the per-XCD replicas (lanes 0..7 of the publishing wave, one store each)
+    if (COH && (threadIdx.x & 63) < kCtlReplicas)
+        __hip_atomic_store(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every replica of Ctl::committed (the persistent pipeline's end and error paths; lanes 0..7)
+__device__ __forceinline__ void publish_committed_all(Ctl *ctl, unsigned long long v) {
+    const int l = threadIdx.x & 63;
+    if (l == 0) __hip_atomic_store(&ctl->committed, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (l < kCtlReplicas) __hip_atomic_store(&ctl->committed_x[l].v, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct alignas(8) PodStage {
@@ -361,9 +379,10 @@ struct PersistArgs {
     // << 32 | low word of the last value a wait saw, busy-time sums}; read by the host when a wait timed out
     // (and by the phase trace)
     uint64_t *prog;
+    int32_t prog_waves;     // KSCHED_PROG_WAVES: every score wave marks its position (prog words 4..11)
 };
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
-constexpr int kProgWords = 4;
+constexpr int kProgWords = 12;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4..11 per-wave marks
 enum : int { kProgWaitCommit = 1, kProgScan = 2, kProgArrived = 3, kProgWaitArrive = 4, kProgMerged = 5,
              kProgWaitMerged = 6, kProgCommitted = 7, kProgIdle = 8, kProgTimedOut = 0x80 };
 __device__ __forceinline__ uint32_t hw_where() {
@@ -379,6 +398,12 @@ __device__ __forceinline__ void prog_at(const PersistArgs &P, int slot, int64_t 
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(P.prog + kProgWords * slot + 1, (uint64_t)hw_where() << 32 | (seen & 0xffffffffull),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// score wave `wave` of workgroup `slot` reached mark `code` of batch b (lane 0; KSCHED_PROG_WAVES only)
+__device__ __forceinline__ void wave_mark(const PersistArgs &P, int slot, int wave, int64_t b, int code) {
+    if (!P.prog_waves || (threadIdx.x & 63) != 0) return;
+    __hip_atomic_store(P.prog + kProgWords * slot + 4 + wave, (uint64_t)b << 8 | (uint64_t)code, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 // busy-time sums of a workgroup (KSCHED_PERSIST_TRACE calls only: P.trace set): word 2 += scan ticks, word 3
 // += ticks from its wait's end to its arrival (word 2 is the heartbeat of a long wait otherwise)

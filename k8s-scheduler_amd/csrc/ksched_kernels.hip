@@ -859,7 +859,9 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     for (int i = 0; i < 5; ++i) ctl->stats[i] = 0;
     ctl->scored = 0;
     ctl->committed = 0;
-    for (int i = 0; i < 4; ++i) { ctl->arrive[i] = 0; ctl->merged[i] = 0; }
+    for (int i = 0; i < 4; ++i) { ctl->arrive[i].v = 0; ctl->merged[i].v = 0; }
+    for (int i = 0; i < kCtlReplicas; ++i) ctl->committed_x[i].v = 0;
+    ctl->polls_rmw = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->cursor_at[i] = 0;
     ctl->nact = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;

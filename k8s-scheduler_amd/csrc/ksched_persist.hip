@@ -138,7 +138,7 @@ __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int
 }  // namespace
 
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
+__global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_num_vgpr(72))) void k_persist_score(PersistArgs P) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     NodeRec *rows = reinterpret_cast<NodeRec *>(smem);                    // [rows_per_wg]
     char *fold = smem + (size_t)P.rows_per_wg * sizeof(NodeRec);
@@ -170,32 +170,38 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
             int stop = 0;
             unsigned long long seen = 0;
             prog_at(P, g, b, kProgWaitCommit, 0);
-            if (b >= 2 && !spin_ge(P, g, &ctl->committed, (unsigned long long)(b - 1), &seen)) {
+            if (b >= 2 && !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
                 set_err(P.err, 6);
                 prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
                 stop = 2;
             }
+            wave_mark(P, g, 0, b, 0x10);  // wave 0: its poll ended
             if (g == 0) trace_at(P, b, 6);
+            // plan, cursor and the export's count of commit(b-2): one round of loads behind the poll
+            const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= 2 ? b - 2 : 0) % 4) * P.xbuf_bytes);
             s_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
             s_done = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+            s_nx = b >= 2 ? (int)(uint32_t)ld_coh(&xb->count) : 0;
             // a failed peer (the commit timed out) ends the call for everyone
             if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
             s_stop = stop;
         }
+        if (tid != 0) wave_mark(P, g, wave, b, 0x01);  // at barrier 1
         __syncthreads();
+        wave_mark(P, g, wave, b, 0x02);  // past barrier 1
         if (s_stop) return;
         const int64_t p0 = s_p0;
         // ---- apply commit(b-2)'s exported nodes to the rows this workgroup owns ----
         if (b >= 2) {
             const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b - 2) % 4) * P.xbuf_bytes);
-            if (tid == 0) s_nx = (int)(uint32_t)ld_coh(&xb->count);
-            __syncthreads();
             const int nx = s_nx;
             for (int e = tid; e < nx; e += kPThreads) {
+                // the entry's node and new state in one round of loads (few workgroups own an entry)
                 const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
-                const int64_t j = (int64_t)(int32_t)(uint32_t)ld_coh(w) - P.node_offset;  // local row
+                const uint64_t w0 = ld_coh(w), w4 = ld_coh(w + 4), w5 = ld_coh(w + 5), w6 = ld_coh(w + 6);
+                const int64_t j = (int64_t)(int32_t)(uint32_t)w0 - P.node_offset;  // local row
                 if (j < 0 || j >= n || j % G != g) continue;  // another rank's node, or another workgroup's
-                const int64_t c0 = (int64_t)ld_coh(w + 4), c1 = (int64_t)ld_coh(w + 5), c2 = (int64_t)ld_coh(w + 6);
+                const int64_t c0 = (int64_t)w4, c1 = (int64_t)w5, c2 = (int64_t)w6;
                 set_row(rows + j / G, c0, c1, c2);
                 // the mergers read a candidate's state from its HBM row (sc1)
                 st_coh(&P.nodes[j].a[0], (uint64_t)c0);
@@ -203,7 +209,9 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
                 st_coh(&P.nodes[j].a[2], (uint64_t)c2);
             }
         }
+        wave_mark(P, g, wave, b, 0x03);  // applied, at barrier 2
         __syncthreads();
+        wave_mark(P, g, wave, b, 0x04);  // past barrier 2
         if (s_done >= NP) break;                  // every pod resolved by commit(b-2) or earlier
         if (p0 < 0 || p0 >= NP) {                 // nothing planned for batch b (identical on every WG)
             if (tid == 0) prog_at(P, g, b, kProgIdle, (uint64_t)p0);
@@ -273,6 +281,7 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
                 }
             }
         }
+        wave_mark(P, g, wave, b, 0x05);  // scanned
         if (g == 0 && tid == 0) trace_at(P, b, 8);
         const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
         __syncthreads();  // s_cnt zeroed before any wave adds
@@ -314,12 +323,13 @@ __global__ __launch_bounds__(kPThreads) void k_persist_score(PersistArgs P) {
             st_coh(part_cnt + (size_t)lane * G + g, (uint64_t)(int64_t)s_cnt[lane]);
         }
         drain_stores();
+        wave_mark(P, g, wave, b, 0x06);  // folded and stored, at the arrive barrier
         __syncthreads();
         // ---- arrive (the merger workgroups, k_persist_merge, wait for all G) ----
         const int slot = (int)((nact - 1) % 4);
         if (tid == 0) {
             if (g == 0) trace_at(P, b, 5);
-            const unsigned long long old = __hip_atomic_fetch_add(&ctl->arrive[slot], 1ull, __ATOMIC_RELAXED,
+            const unsigned long long old = __hip_atomic_fetch_add(&ctl->arrive[slot].v, 1ull, __ATOMIC_RELAXED,
                                                                   __HIP_MEMORY_SCOPE_AGENT);
             const unsigned long long use = (unsigned long long)((nact - 1) / 4);
             if (old + 1 == (use + 1) * (unsigned long long)G) trace_at(P, b, 1);
@@ -359,7 +369,7 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
             int stop = 0;
             unsigned long long seen = 0;
             prog_at(P, P.G + m, b, kProgWaitCommit, 0);
-            if (b >= 2 && !spin_ge(P, P.G + m, &ctl->committed, (unsigned long long)(b - 1), &seen)) {
+            if (b >= 2 && !spin_ge(P, P.G + m, &ctl->committed_x[m % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
                 set_err(P.err, 6);
                 prog_at(P, P.G + m, b, kProgWaitCommit | kProgTimedOut, seen);
                 stop = 2;
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
         if (tid == 0) {
             unsigned long long seen = 0;
             prog_at(P, G + m, b, kProgWaitArrive, 0);
-            s_stop = spin_ge(P, G + m, &ctl->arrive[slot], (use + 1) * (unsigned long long)G, &seen) ? 0 : 1;
+            s_stop = spin_ge(P, G + m, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, &seen) ? 0 : 1;
             if (s_stop) {
                 set_err(P.err, 7);
                 prog_at(P, G + m, b, kProgWaitArrive | kProgTimedOut, seen);
@@ -450,7 +460,7 @@ __global__ __launch_bounds__(kMergeThreads) __attribute__((amdgpu_num_vgpr(56)))
         if (tid == 0 && m == 0) st_coh(&ctl->nact, (uint64_t)nact);
         if (tid == 0) {
             const unsigned long long d =
-                __hip_atomic_fetch_add(&ctl->merged[slot], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(&ctl->merged[slot].v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (d + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
             prog_at(P, G + m, b, kProgMerged, d + 1);
         }
