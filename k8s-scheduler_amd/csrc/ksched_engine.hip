@@ -582,8 +582,11 @@ int enqueue_persistent(ksched_ctx *c) {
     const int64_t n_geom = c->xchg_run ? std::max<int64_t>(n, (c->n_global + c->o.nranks - 1) / c->o.nranks) : n;
     // workgroups of a launch go round-robin to the 8 XCDs (32 CUs each), so the grid must leave one CU
     // free on EVERY XCD for the commit workgroup to be guaranteed a place: G <= CUs - 8 (measured: with
-    // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts)
-    const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - kXcds));
+    // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts).  The default leaves TWO
+    // per XCD: at G = CUs - 8 the commit's XCD is full, and in about one c4 call in twenty the last two score
+    // workgroups dispatched to it stalled inside their export apply for seconds (per-wave marks, DESIGN.md
+    // section 4.1); at CUs - 16 none did in 60 calls (c4 1.61e11 -> 1.56e11 evals/s).
+    const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - 2 * kXcds));
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n_geom + 15) / 16));
     if (G > c->cus - kXcds) return 1;
     const int R = (int)((n_geom + G - 1) / G);
