@@ -587,7 +587,9 @@ int enqueue_persistent(ksched_ctx *c) {
     // workgroups dispatched to it stalled inside their export apply for seconds (per-wave marks, DESIGN.md
     // section 4.1); at CUs - 16 none did in 60 calls (c4 1.61e11 -> 1.56e11 evals/s).
     const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - 2 * kXcds));
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n_geom + 15) / 16));
+    // at least ~96 rows per workgroup: a smaller grid costs scan time but every list fewer shortens the merge
+    // (one rank's share of an 8-GPU c4, 12.5k nodes: G = 128 -> 22.8 us per batch, 240 -> 23.8, 64 -> 24.6)
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n_geom + 95) / 96));
     if (G > c->cus - kXcds) return 1;
     const int R = (int)((n_geom + G - 1) / G);
     const size_t lds = persist_score_lds(KC, R);
