@@ -55,25 +55,6 @@ __device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb
     return ca > cb || (ca == cb && ia < ib);
 }
 
-// how many of the N (code, idx) pairs at c[], x[] (16-byte aligned, N % 4 == 0) rank above (mc, mi):
-// 4 pairs per step with two 16-byte code reads and one 16-byte index read (broadcast LDS reads)
-template <int N>
-__device__ __forceinline__ int rank_in(const uint64_t *c, const int32_t *x, uint64_t mc, int32_t mi) {
-    static_assert(N % 4 == 0, "rank_in: N % 4");
-    int r = 0;
-#pragma unroll 4
-    for (int t = 0; t < N; t += 4) {
-        const ulonglong2 ca = *reinterpret_cast<const ulonglong2 *>(c + t);
-        const ulonglong2 cb = *reinterpret_cast<const ulonglong2 *>(c + t + 2);
-        const int4 xi = *reinterpret_cast<const int4 *>(x + t);
-        r += code_better(ca.x, xi.x, mc, mi) ? 1 : 0;
-        r += code_better(ca.y, xi.y, mc, mi) ? 1 : 0;
-        r += code_better(cb.x, xi.z, mc, mi) ? 1 : 0;
-        r += code_better(cb.y, xi.w, mc, mi) ? 1 : 0;
-    }
-    return r;
-}
-
 template <int KC, int K, bool COH = false>
 __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
     // latency-critical: win issue arbitration over co-resident score waves (low_prio: yield to them)
@@ -81,14 +62,11 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
     constexpr int W = kMergeThreads / 64;
     __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
     __shared__ int32_t s_idx[kMergeThreads][KC];
-    __shared__ __attribute__((aligned(16))) uint64_t s_hcode[kMergeThreads];  // list heads, contiguous: the
-    __shared__ __attribute__((aligned(16))) int32_t s_hidx[kMergeThreads];    // rank loops read 4 per step
-    __shared__ __attribute__((aligned(16))) uint64_t s_ccode[W * K];  // surviving heads
-    __shared__ __attribute__((aligned(16))) int32_t s_cidx[W * K];
-    __shared__ int32_t s_clist[W * K];
+    __shared__ uint64_t s_ccode[W * K];             // surviving heads
+    __shared__ int32_t s_cidx[W * K], s_clist[W * K];
     __shared__ int32_t s_keep[K];                   // list of global head rank g
-    __shared__ __attribute__((aligned(16))) uint64_t s_ecode[K * KC];  // the kept lists' entries
-    __shared__ __attribute__((aligned(16))) int32_t s_eidx[K * KC];
+    __shared__ uint64_t s_ecode[K * KC];            // the kept lists' entries
+    __shared__ int32_t s_eidx[K * KC];
     __shared__ uint64_t s_ocode[K];
     __shared__ int32_t s_oidx[K];
     __shared__ uint64_t s_wck[W];
@@ -129,8 +107,6 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
     }
 #pragma unroll
     for (int q = 0; q < KC; ++q) { s_code[tid][q] = code[q]; s_idx[tid][q] = idx[q]; }
-    s_hcode[tid] = code[0];
-    s_hidx[tid] = idx[0];
     if (tid < W * K) { s_ccode[tid] = 0ull; s_cidx[tid] = kNoIdx; }  // empty survivor slots never rank
     if (dbg) { asm volatile("" ::"v"(code[0]), "v"(cnt)); ts[1] = __builtin_amdgcn_s_memtime(); }
     // wave partials: best cutoff (last entry of a full list), count, cut flag
@@ -149,8 +125,11 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
     // 1. rank each head within its wave (broadcast reads, independent compares; waves without lists idle)
     const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
     if (wave < nw) {
+        int rank = 0;
         const int base = wave * 64;
-        const int rank = rank_in<64>(s_hcode + base, s_hidx + base, code[0], idx[0]);
+#pragma unroll 16
+        for (int t = 0; t < 64; ++t)
+            rank += code_better(s_code[base + t][0], s_idx[base + t][0], code[0], idx[0]) ? 1 : 0;
         if (idx[0] != kNoIdx && rank < K) {
             s_ccode[wave * K + rank] = code[0];
             s_cidx[wave * K + rank] = idx[0];
@@ -170,7 +149,8 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
             const uint64_t mc = s_ccode[tid];
             const int32_t mi = s_cidx[tid];
             int g = 0;
-            for (int c0 = 0; c0 < nw * K; c0 += K) g += rank_in<K>(s_ccode + c0, s_cidx + c0, mc, mi);
+#pragma unroll 16
+            for (int c = 0; c < nw * K; ++c) g += code_better(s_ccode[c], s_cidx[c], mc, mi) ? 1 : 0;
             if (g < K) s_keep[g] = s_clist[tid];
         }
     }
@@ -191,7 +171,9 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         const uint64_t mc = s_ecode[tid];
         const int32_t mi = s_eidx[tid];
         if (mi != kNoIdx) {
-            const int r = rank_in<K * KC>(s_ecode, s_eidx, mc, mi);
+            int r = 0;
+#pragma unroll 16
+            for (int e = 0; e < K * KC; ++e) r += code_better(s_ecode[e], s_eidx[e], mc, mi) ? 1 : 0;
             if (r < K) { s_ocode[r] = mc; s_oidx[r] = mi; }
         }
     }
