@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_num_vgpr(72))) voi
     int32_t *s_idx = reinterpret_cast<int32_t *>(fold + (size_t)(kPW / 2) * KC * 64 * 8);
     int32_t *s_cnt = s_idx + (size_t)(kPW / 2) * KC * 64;                 // [64]
     __shared__ int64_t s_p0, s_done;
-    __shared__ int s_stop, s_nx;
+    __shared__ int s_stop;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -165,53 +165,66 @@ __global__ __launch_bounds__(kPThreads) __attribute__((amdgpu_num_vgpr(72))) voi
     int64_t nact = 0;
     int idle = 0;
     for (int64_t b = 0;; ++b) {
-        // ---- wait for commit(b-2): its plan for b, its exported commits, the cursor after it ----
-        if (tid == 0) {
+        // ---- wave 0: wait for commit(b-2), then ONE round of loads -- its plan for b, the cursor after it,
+        // its export (count and entries, lane = entry) -- and apply the exported nodes this workgroup owns
+        // to its LDS rows before the barrier (the other waves never touch the export) ----
+        if (wave == 0) {
             int stop = 0;
-            unsigned long long seen = 0;
-            prog_at(P, g, b, kProgWaitCommit, 0);
-            if (b >= 2 && !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
-                set_err(P.err, 6);
-                prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
-                stop = 2;
+            if (lane == 0) {
+                unsigned long long seen = 0;
+                prog_at(P, g, b, kProgWaitCommit, 0);
+                if (b >= 2 && !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
+                    set_err(P.err, 6);
+                    prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
+                    stop = 2;
+                }
+                if (g == 0) trace_at(P, b, 6);
             }
+            stop = __builtin_amdgcn_readfirstlane(stop);
             wave_mark(P, g, 0, b, 0x10);  // wave 0: its poll ended
-            if (g == 0) trace_at(P, b, 6);
-            // plan, cursor and the export's count of commit(b-2): one round of loads behind the poll
+            int64_t p0v = 0, donev = 0;
+            int errv = 0, nxv = 0;
+            uint64_t w0 = 0, w4 = 0, w5 = 0, w6 = 0;
             const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= 2 ? b - 2 : 0) % 4) * P.xbuf_bytes);
-            s_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
-            s_done = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
-            s_nx = b >= 2 ? (int)(uint32_t)ld_coh(&xb->count) : 0;
-            // a failed peer (the commit timed out) ends the call for everyone
-            if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
-            s_stop = stop;
+            if (lane == 0) {
+                p0v = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+                donev = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+                // a failed peer (the commit timed out) ends the call for everyone
+                errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (b >= 2) {
+                nxv = (int)(uint32_t)ld_coh(&xb->count);  // one address: one request for the wave
+                if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
+                    const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[lane]);
+                    w0 = ld_coh(w); w4 = ld_coh(w + 4); w5 = ld_coh(w + 5); w6 = ld_coh(w + 6);
+                }
+            }
+            auto apply = [&](uint64_t x0, uint64_t x4, uint64_t x5, uint64_t x6) {
+                const int64_t j = (int64_t)(int32_t)(uint32_t)x0 - P.node_offset;  // local row
+                if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
+                set_row(rows + j / G, (int64_t)x4, (int64_t)x5, (int64_t)x6);
+                // the mergers read a candidate's state from its HBM row (sc1)
+                st_coh(&P.nodes[j].a[0], x4);
+                st_coh(&P.nodes[j].a[1], x5);
+                st_coh(&P.nodes[j].a[2], x6);
+            };
+            if (lane < nxv) apply(w0, w4, w5, w6);
+            for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
+                const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
+                apply(ld_coh(w), ld_coh(w + 4), ld_coh(w + 5), ld_coh(w + 6));
+            }
+            if (lane == 0) {
+                s_p0 = p0v;
+                s_done = donev;
+                s_stop = errv != 0 ? 3 : stop;
+            }
+        } else {
+            wave_mark(P, g, wave, b, 0x01);  // at barrier 1
         }
-        if (tid != 0) wave_mark(P, g, wave, b, 0x01);  // at barrier 1
         __syncthreads();
-        wave_mark(P, g, wave, b, 0x02);  // past barrier 1
+        wave_mark(P, g, wave, b, 0x02);  // past barrier 1 (rows up to date)
         if (s_stop) return;
         const int64_t p0 = s_p0;
-        // ---- apply commit(b-2)'s exported nodes to the rows this workgroup owns ----
-        if (b >= 2) {
-            const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b - 2) % 4) * P.xbuf_bytes);
-            const int nx = s_nx;
-            for (int e = tid; e < nx; e += kPThreads) {
-                // the entry's node and new state in one round of loads (few workgroups own an entry)
-                const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
-                const uint64_t w0 = ld_coh(w), w4 = ld_coh(w + 4), w5 = ld_coh(w + 5), w6 = ld_coh(w + 6);
-                const int64_t j = (int64_t)(int32_t)(uint32_t)w0 - P.node_offset;  // local row
-                if (j < 0 || j >= n || j % G != g) continue;  // another rank's node, or another workgroup's
-                const int64_t c0 = (int64_t)w4, c1 = (int64_t)w5, c2 = (int64_t)w6;
-                set_row(rows + j / G, c0, c1, c2);
-                // the mergers read a candidate's state from its HBM row (sc1)
-                st_coh(&P.nodes[j].a[0], (uint64_t)c0);
-                st_coh(&P.nodes[j].a[1], (uint64_t)c1);
-                st_coh(&P.nodes[j].a[2], (uint64_t)c2);
-            }
-        }
-        wave_mark(P, g, wave, b, 0x03);  // applied, at barrier 2
-        __syncthreads();
-        wave_mark(P, g, wave, b, 0x04);  // past barrier 2
         if (s_done >= NP) break;                  // every pod resolved by commit(b-2) or earlier
         if (p0 < 0 || p0 >= NP) {                 // nothing planned for batch b (identical on every WG)
             if (tid == 0) prog_at(P, g, b, kProgIdle, (uint64_t)p0);
