@@ -1389,7 +1389,7 @@ int ksched_sync(ksched_ctx *c) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
         static const char *what[] = {"the commit's wait for the merges", "a score workgroup's wait for commit(b-2)",
                                      "a merger's wait for the score workgroups", "the score grid's plan (idle)",
-                                     "the commit's plan (idle)", "(unused)",
+                                     "the commit's plan (idle)",
                                      "a merger's wait for a peer rank's candidate lists (node-sharded exchange)",
                                      "the ranks' device barrier (node-sharded exchange)"};
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
