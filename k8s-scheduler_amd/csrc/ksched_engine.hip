@@ -277,7 +277,7 @@ int decide_fast53(ksched_ctx *c) {
         PersistArgs a{};
         fill_xchg_args(c, &a);
         a.err = c->d_err;
-        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 2000) * 100000;
+        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
         int32_t mn = -1;
         HIPCHK(c, launch_xchg_min(a, flag, c->d_xmin, c->stream));
         HIPCHK(c, hipMemcpyAsync(&mn, c->d_xmin, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -635,7 +635,7 @@ int enqueue_persistent(ksched_ctx *c) {
     a.err = c->d_err;
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)
-    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 2000) * 100000;
+    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
     if (env_int("KSCHED_PERSIST_TRACE", 0)) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {

@@ -15,7 +15,7 @@ def run_rank(rank, world, port, cfg, nn, pp, calls, q):
         # its share of the CUs, leaving enough free CUs that every rank's commit workgroup (exclusive CU)
         # still finds one after the other ranks' mergers (up to two per free CU) have landed
         os.environ["KSCHED_PERSIST_G"] = str(max(8, (256 - 34 * world) // world // 8 * 8))
-        os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "5000")
+        os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "20000")
         import numpy as np
         import torch.distributed as dist
         from ksched import MODE_BATCHED, cluster
