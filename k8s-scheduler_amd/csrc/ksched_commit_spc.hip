@@ -746,6 +746,7 @@ __global__ __launch_bounds__(kSpcThreads) void k_persist_commit(PersistArgs P) {
         ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
         ca.dbg = P.cdbg;
         ca.loc = &loc;
+        ca.release = P.commit_release;
         if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true>(ca, smem, &pre, wait_merged)) {
             if (threadIdx.x == 0) atomicCAS(P.err, 0, 5);
             if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);

@@ -632,6 +632,7 @@ int enqueue_persistent(ksched_ctx *c) {
     fill_xchg_args(c, &a);
     a.merge_low_prio = env_int("KSCHED_MERGE_LOW_PRIO", 0);
     a.prog_waves = env_int("KSCHED_PROG_WAVES", 0);
+    a.commit_release = env_int("KSCHED_COMMIT_RELEASE", 0);
     a.err = c->d_err;
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)

@@ -218,6 +218,7 @@ struct CommitArgs {
     int64_t batch;          // this batch's index in the call (published to Ctl::committed when done)
     int64_t *cursor_at;     // persistent pipeline: &Ctl::cursor_at[batch % kPlanRing] (else null)
     PersistLocal *loc;      // persistent pipeline (COH): the commit workgroup's LDS control state
+    int32_t release;        // COH: also write back the XCD's L2 (agent release) before Ctl::committed
 };
 
 // Commit(b) -> score(b+2) hand-off on the device: the committing wave drains its stores, writes back the
@@ -231,7 +232,7 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
         st_coh(A.cursor_at, COH ? (uint64_t)A.loc->cursor : ld_coh(&A.ctl->cursor));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((threadIdx.x & 63) == 0) {
-        if (!COH) {
+        if (!COH || A.release) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -380,6 +381,7 @@ struct PersistArgs {
     // (and by the phase trace)
     uint64_t *prog;
     int32_t prog_waves;     // KSCHED_PROG_WAVES: every score wave marks its position (prog words 4..11)
+    int32_t commit_release; // KSCHED_COMMIT_RELEASE: agent release (L2 write-back) before each publication
 };
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
 constexpr int kProgWords = 12;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4..11 per-wave marks
