@@ -57,8 +57,14 @@ __device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb
 
 template <int KC, int K, bool COH = false>
 __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
-    // latency-critical: win issue arbitration over co-resident score waves (low_prio: yield to them)
-    if (A.low_prio) __builtin_amdgcn_s_setprio(0); else __builtin_amdgcn_s_setprio(3);
+    // latency-critical: win issue arbitration over co-resident score waves (low_prio 1/2/3: issue priority
+    // 0/1/2 instead of 3, A/B of how much the merge may take from the score waves sharing its SIMDs)
+    switch (A.low_prio) {
+        case 1: __builtin_amdgcn_s_setprio(0); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        case 3: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
     constexpr int W = kMergeThreads / 64;
     __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
     __shared__ int32_t s_idx[kMergeThreads][KC];
