@@ -28,7 +28,7 @@ FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-s
 # PMC summaries of the same workloads (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ
 # passes of `bench.py` itself); keyed by (kernel, config, batch, ranks)
 PMC_SUMMARIES = {
-    ("k_persist_score", "c4", 64, 1): os.path.join(ROOT, "profiles", "r02_pmc_c4_persist.json"),
+    ("k_pipe", "c4", 64, 1): os.path.join(ROOT, "profiles", "r03_pmc_c4_pipe.json"),
     ("k_score_topk", "c4", 64, 1): os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json"),
 }
 
@@ -140,7 +140,6 @@ def main():
         # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, each grid on its share of
         # the CUs, torch.distributed over gloo, no RCCL communicator (RCCL refuses two ranks per GPU)
         local = 0
-        os.environ.setdefault("KSCHED_PERSIST_G", str(max(8, (256 - 34 * world) // world // 8 * 8)))
     tdev = "cpu" if args.same_device else "cuda"
     if world > 1:
         import torch
@@ -160,7 +159,8 @@ def main():
     # communicator kept as the fallback transport (stream pipeline, one all-gather per batch)
     eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=local, mode=mode, topk=args.topk,
                                         batch=args.batch, timing=False, xchg=world > 1 and not args.no_xchg,
-                                        comm=not args.same_device)
+                                        comm=not args.same_device,
+                                        pipe_wgs=(256 - 8) // world if args.same_device else 0)
     eng.save_state()
     eng.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
 
@@ -174,41 +174,11 @@ def main():
         return eng.results()
 
     step_stats = []
-    fallbacks = []
-
-    def guarded_step():
-        """step(); if the persistent pipeline reports a device timeout (every wait in it is bounded), the
-        same step is redone on the stream pipeline -- inside the timed region, so the lost time counts --
-        and the failure is reported in the JSON line.  Ranks agree on it (N > 1)."""
-        from ksched import KschedError
-        err = None
-        try:
-            r = step()
-        except KschedError as ex:
-            err, r = str(ex), None
-        if dist is not None:
-            t = torch.tensor([0 if err else 1], dtype=torch.int32, device=tdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
-            failed = int(t.item()) == 0
-        else:
-            failed = err is not None
-        if not failed:
-            return r
-        fallbacks.append(err or "a peer rank failed")
-        print(f"rank {rank}: persistent pipeline failed ({err}); redoing the step on the stream pipeline",
-              file=sys.stderr, flush=True)
-        os.environ["KSCHED_PERSIST"] = "0"
-        os.environ["KSCHED_XCHG"] = "0"
-        try:
-            return step()
-        finally:
-            os.environ.pop("KSCHED_PERSIST", None)
-
+    from ksched import KschedError
     for w in range(max(args.warmup, 1 if world > 1 else 0)):
         if world > 1 and w == 0:
-            # every rank must take the same transport: if the exchange failed anywhere (a device
-            # timeout), all ranks fall back to the RCCL stream pipeline together
-            from ksched import KschedError
+            # every rank must take the same transport: if the device exchange failed anywhere (a device
+            # timeout), every rank turns it off (ksched_xchg_close) and the RCCL stream pipeline runs
             ok = 1
             try:
                 step()
@@ -218,10 +188,10 @@ def main():
             t = torch.tensor([ok], dtype=torch.int32, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MIN)
             if int(t.item()) == 0:
-                os.environ["KSCHED_XCHG"] = "0"
+                eng.xchg_close()
                 step()
         else:
-            guarded_step()
+            step()
     pipeline = eng.stats()["pipeline"]
     persistent = pipeline == "persistent"
     # the persistent pipeline is ONE score-grid launch per step: its HIP events (on the grid's own
@@ -234,9 +204,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        nf = len(fallbacks)
-        res = guarded_step()
-        if persistent and len(fallbacks) == nf:
+        res = step()
+        if persistent:
             step_stats.append(eng.stats())
     torch.cuda.synchronize()
     if dist is not None:
@@ -255,10 +224,10 @@ def main():
         kstats = step_stats
     else:
         eng.set_timing(True, 8)
-        guarded_step()
+        step()
         kstats = [eng.stats()]
         eng.set_timing(False)
-    names = (["k_exact"] if mode == MODE_EXACT else ["k_persist_score" if persistent else "k_score_topk"]) + \
+    names = (["k_exact"] if mode == MODE_EXACT else ["k_pipe" if persistent else "k_score_topk"]) + \
         ["k_merge", "k_commit", "rccl_allgather+merge"]
     fam_ms = [sum(s["kernel_ms"][f] for s in kstats) for f in range(4)]
     fam_n = [sum(s["kernel_launches"][f] for s in kstats) for f in range(4)]
@@ -281,7 +250,7 @@ def main():
         "pairs_per_launch": score_pairs_per_launch,
         "avg_launch_ms": score_avg_ms,
         "launches_timed": fam_n[0],
-        "timing": "HIP events on the score grid's stream, inside the timed steps" if persistent else
+        "timing": "HIP events on the kernel's stream, inside the timed steps" if persistent else
                   "HIP events on the score stream, one batch in 8 of one untimed pass",
     }
     if pmc:
@@ -330,8 +299,6 @@ def main():
         "kernel_avg_ms": fam_share,
         "roofline": roof,
     }
-    if fallbacks:
-        out["persistent_failures"] = fallbacks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         base, mt = cpu_baseline(cl, args.cpu_baseline_s)
         out["cpu_baseline"] = base

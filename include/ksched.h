@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 3
+#define KSCHED_ABI_VERSION 4
 
 /* status codes */
 #define KSCHED_OK 0
@@ -53,6 +53,10 @@ extern "C" {
 #define KSCHED_COMMIT_LANE_PER_POD 2  /* retired (round 1 variant): treated as KSCHED_COMMIT_SPECULATIVE */
 #define KSCHED_COMMIT_SPECULATIVE 3   /* guess first touches, check all pods in parallel, resolve the first miss (batch <= 64) */
 
+/* batched-mode pipelines (all produce the same results) */
+#define KSCHED_PIPELINE_AUTO 0    /* the persistent kernel where the configuration fits it, else the stream pipeline */
+#define KSCHED_PIPELINE_STREAM 1  /* always the stream pipeline (per-batch score / merge / commit launches) */
+
 #define KSCHED_DOMAIN_ALL 0       /* argmax over ALL nodes, feasible or not (the reference, anchor/priorities.go:45) */
 #define KSCHED_DOMAIN_FEASIBLE 1  /* argmax over feasible nodes only (build extension) */
 
@@ -76,7 +80,11 @@ typedef struct ksched_opts {
     int32_t chunk_topk;   /* batched mode: candidates kept per node chunk before the merge, 2/4/8/16 (0 = auto);
                              capped at topk.  The merge keeps the exact prefix. */
     int32_t commit_impl;  /* batched mode: KSCHED_COMMIT_* (0 = auto: speculative when batch <= 64) */
-    int32_t reserved[3];
+    int32_t pipeline;     /* batched mode: KSCHED_PIPELINE_AUTO (0) or KSCHED_PIPELINE_STREAM (ABI 4) */
+    int32_t pipe_wgs;     /* persistent pipeline: at most this many workgroups, one per CU (0 = every CU).
+                             Ranks that share ONE device (a test rehearsal of the multi-GPU path) split its
+                             CUs with it; the launch is then a plain one instead of a cooperative one. (ABI 4) */
+    int32_t reserved[1];
 } ksched_opts;
 
 typedef struct ksched_ctx ksched_ctx;
@@ -100,7 +108,7 @@ enum {
     KSCHED_PIPE_EXACT = 1,      /* the exact persistent kernel, one pod at a time */
     KSCHED_PIPE_STREAM = 2,     /* batched: score / merge / speculative commit kernels per batch, stream-linked */
     KSCHED_PIPE_STREAM_SEQ = 3, /* batched with the sequential one-pod-at-a-time commit kernel */
-    KSCHED_PIPE_PERSISTENT = 4  /* batched single-rank: resident score grid + resident commit workgroup */
+    KSCHED_PIPE_PERSISTENT = 4  /* batched: ONE persistent kernel (commit workgroup + score/merge workgroups) */
 };
 
 /* ---- lifecycle ---- */
@@ -136,6 +144,9 @@ int ksched_set_comm(ksched_ctx *ctx, const uint8_t id[128]);
 int ksched_xchg_export(ksched_ctx *ctx, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]);
 int ksched_xchg_import(ksched_ctx *ctx, const uint8_t *handles);
 int ksched_xchg_ready(const ksched_ctx *ctx);
+/* Turns the exchange off on this rank (later batched calls take the RCCL path).  Every rank calls it when
+ * any rank failed to import (ABI 4): the ranks must agree on the transport. */
+int ksched_xchg_close(ksched_ctx *ctx);
 
 typedef struct ksched_group ksched_group;
 int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out);
@@ -197,6 +208,10 @@ int ksched_schedule(ksched_ctx *ctx, int64_t p, const int64_t *req_cpu, const in
 int ksched_upload_pods(ksched_ctx *ctx, int64_t p, const int64_t *req_cpu, const int64_t *req_mem,
                        const int64_t *req_pods, const uint64_t *selector);
 int ksched_run(ksched_ctx *ctx);                 /* schedules the staged pods; results stay on device */
+/* Bound of every device-side wait of the persistent pipeline, in ms (default 10000, or the
+ * KSCHED_PERSIST_TIMEOUT_MS environment variable at create).  A wait that exceeds it ends the call with
+ * KSCHED_E_DEVICE naming the wait and where every workgroup stood (ABI 4). */
+int ksched_set_timeout(ksched_ctx *ctx, int32_t persist_ms);
 int ksched_sync(ksched_ctx *ctx);                /* waits for the run; fills stats */
 int ksched_download_results(ksched_ctx *ctx, int64_t p, int32_t *out_idx, double *out_score, int32_t *out_feasible);
 int ksched_get_stats(const ksched_ctx *ctx, ksched_stats *out);

@@ -1,0 +1,668 @@
+// ksched_commit.h -- the ordered commit of one speculative batch (speculation + parallel check), shared by
+// the stream pipeline's k_commit_spc (ksched_commit_spc.hip) and the commit workgroup of the persistent
+// pipeline (ksched_pipe.hip).
+//
+// Same result as the sequential replay (k_commit): pods of the batch
+// in order, each seeing every placement before it (anchor/schedule.go:185-197).  Instead of deciding
+// one pod at a time, a round
+//   1. (wave 0, integer work only) GUESSES every remaining pod's placement: its first list entry that
+//      is neither touched nor guessed by an earlier pod of the round ("first touch"), or none when the
+//      pod has no feasible node or its list is exhausted;
+//   2. (all 16 waves) evaluates the guesses in parallel: for every guessed node, its state after the
+//      guessing pod's commit, and every pod's exact key and predicate delta against that state;
+//   3. (wave 0, lane = pod) checks each pod's exact sequential decision under the guesses of the pods
+//      before it: fc = predicate count, t* = best touched node (confirmed + guessed before it), u* =
+//      its guess.  The guesses up to the first pod whose decision differs are the sequential outcome
+//      (induction from the round's start); that pod is resolved exactly and the next round starts
+//      after it.
+// Placements are first touches almost always (99.4 % on BASELINE c4), so a batch usually takes one or
+// two rounds.  The guess window adapts (halves around failures) to bound the cost of adversarial
+// batches.  The lists, cut rule, touched-set inheritance, export, plan and truncation are those of
+// k_commit.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ksched_kernels.h"
+
+namespace ksched {
+
+namespace {
+
+constexpr int kSpcHashBits = 11;  // touched + guessed node set (stale guesses stay until re-tagged)
+constexpr int kSpcHash = 1 << kSpcHashBits;
+constexpr int kSpcSlots = 128;    // previous batch's commits (<= 64) + this batch's (<= 64)
+constexpr int kSpcRow = kSpcSlots + 1;
+constexpr int kSpcInvalid = kSpcHash - 1;  // table position reserved for "no entry" (always taken)
+
+struct alignas(8) SpcSlot {
+    int32_t idx;
+    int32_t mine;     // committed by this batch (exported)
+    int64_t s0[3];    // state at this batch's score snapshot
+    int64_t sb[3];    // state when this batch's commit started
+    int64_t cur[3];   // current state
+    uint64_t labels;
+    float price;
+    int32_t pad;
+};
+static_assert(sizeof(SpcSlot) == 96, "SpcSlot");
+
+struct SpcSmem {
+    int32_t *hk;      // open-addressed table: node index per position (-1 = empty)
+    int32_t *HP;      // [K][64] table position of list entry (q, pod); kSpcInvalid for no entry
+    uint32_t *tkc;    // [64] words: bit = position taken by a CONFIRMED touch (T)
+    int32_t *ti;      // node index per slot
+    SpcSlot *T;
+    double *S;        // [64 pods][kSpcRow] key of (pod, slot), -inf = not eligible
+    double *LK;       // [K][64] list keys (lane-contiguous)
+    int32_t *LI;      // [K][64] list node indices
+    int8_t *D;        // [64 guessing pods][64 pods] predicate delta of the guessed commit
+    int32_t *fcg;     // per pod: sum of D over this round's guesses before it
+    int32_t *dfacc;   // per pod: predicate delta of the inherited slots
+    int32_t *gn;      // per pod: guessed node (>= 0), -1 list exhausted, -2 predicted no fit
+    int32_t *gq;      // per pod: list position of the guess
+    int32_t *gs;      // per pod: slot of the guess
+    double *pbk;      // [16 waves][64 pods] partial best key over the wave's guessed columns
+    int64_t *pbx;     // [16 waves][64 pods] (slot << 32) | node of that best
+    int32_t *ctl;     // [0] round start c, [1] window end, [2] stop
+    int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none)
+    uint64_t *GS;     // [64 pods][5] node state words (a[3], labels, price) of each pod's guessed entry
+};
+
+__device__ __forceinline__ uint32_t spc_hash(int32_t idx) {
+    return ((uint32_t)idx * 2654435761u) >> (32 - kSpcHashBits);
+}
+
+// Node -> position in an open-addressed table of every node the batch can touch (list entries and
+// inherited slots).  The position is a compact node id: "taken" is one bit per position.
+__device__ __forceinline__ int spc_pos_insert(int32_t *hk, int32_t idx) {
+    uint32_t h = spc_hash(idx);
+    for (;;) {
+        if (h != kSpcInvalid) {
+            const int32_t prev = atomicCAS(&hk[h], -1, idx);
+            if (prev == -1 || prev == idx) return (int)h;
+        }
+        h = (h + 1) & (kSpcHash - 1);
+    }
+}
+
+__device__ __forceinline__ int64_t rl64(int64_t v, int src) {
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)((uint64_t)v >> 32), src);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)v, src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// plan_after_commit for the persistent commit: the plans come from (and go to) its LDS copy too
+__device__ __forceinline__ void persist_plan(const CommitArgs &A, bool truncated, int64_t cursor) {
+    PersistLocal *L = A.loc;
+    const int64_t n1 = L->plan[(A.batch + 1) % kPlanRing];
+    int64_t nx = truncated ? cursor : (n1 < 0 ? -1 : n1 + A.B);
+    if (nx >= A.pods.p) nx = -1;
+    L->plan[(A.batch + 2) % kPlanRing] = nx;
+    st_coh(A.plan2, (uint64_t)nx);
+}
+
+__device__ __forceinline__ void lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// pod (this lane)'s exact key against a node state; -inf when not eligible
+template <int PRIO, int DOM, bool LAB, bool F53>
+__device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64_t rp, double rcf, double rmf,
+                                           double rpf, int64_t n0, int64_t n1, int64_t n2, double y3, float pr) {
+    const double nf0 = (double)n0, nf1 = (double)n1, nf2 = (double)n2;
+    const double ny0 = recip_or_zero(n0, nf0), ny1 = recip_or_zero(n1, nf1), ny2 = recip_or_zero(n2, nf2);
+    double k;
+    const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, nf0, nf1, nf2, ny0, ny1,
+                                                  ny2, y3, pr, &k);
+    return el ? k : -__builtin_inf();
+}
+
+}  // namespace
+
+// One batch's ordered commit by the whole workgroup (kSpcThreads).  COH: the lists arrive from other
+// workgroups of a running persistent kernel (sc1 loads), and what the score workgroups read back --
+// the XBuf export, the next plans, the cursor -- leaves as sc1 stores (ksched_persist.hip).
+// a batch's pod requests, lane = pod (loaded early by the persistent commit, before its wait)
+struct LanePods {
+    int64_t rc, rm, rp;
+    uint64_t sel;
+};
+
+template <bool LAB>
+__device__ __forceinline__ LanePods load_lane_pods(const PodArgs &pods, int64_t p0, int nb) {
+    const int lane = threadIdx.x & 63;
+    const bool pj = lane < nb;
+    LanePods q;
+    q.rc = pj ? pods.rc[p0 + lane] : 0;
+    q.rm = pj ? pods.rm[p0 + lane] : 0;
+    q.rp = pj ? pods.rp[p0 + lane] : 0;
+    q.sel = (LAB && pj) ? pods.sel[p0 + lane] : 0;
+    return q;
+}
+
+struct NoWait {
+    __device__ bool operator()() const { return true; }
+};
+
+// wait(): called by every thread once the work that needs no candidate list is done (the persistent
+// commit waits there for the batch's merges); false = give up (the caller reports the timeout).
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH, int NT = kSpcThreads, typename Wait = NoWait>
+__device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr,
+                                                 Wait wait = Wait{}) {
+    constexpr int kSpcWaves = NT / 64;
+    constexpr int kSpcThreads = NT;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    PersistLocal *const L = A.loc;
+    const int64_t p0 = COH ? L->plan[A.batch % kPlanRing] : load_i64<COH>(A.plan);
+    const int64_t cursor = COH ? L->cursor : load_i64<COH>(&A.ctl->cursor);
+    if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
+        if (!wait()) return false;
+        // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
+        if (wave == 0) {
+            if (lane == 0) {
+                if (COH) {
+                    st_coh(&A.xout->count, 0ull);
+                    L->xcount = 0;
+                    if (p0 >= 0 && p0 < A.pods.p) st_coh(&A.ctl->stats[3], (uint64_t)++L->stats[3]);
+                    persist_plan(A, false, cursor);
+                } else {
+                    A.xout->count = 0;
+                    if (p0 >= 0 && p0 < A.pods.p) add_i64<COH>(&A.ctl->stats[3], 1);
+                    plan_after_commit<COH>(A, false, cursor);
+                }
+            }
+            publish_committed<COH>(A);
+        }
+        return true;
+    }
+    const bool dbg = A.dbg != nullptr;  // diagnostics build of the phase timing (KSCHED_COMMIT_STAMPS)
+    uint64_t t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t t_pre = 0;
+    uint64_t t_s1 = 0, t_s2 = 0, t_s3 = 0, t_mark = 0;
+    SpcSmem m;
+    {
+        char *p = smem;
+        m.S = reinterpret_cast<double *>(p); p += (size_t)64 * kSpcRow * sizeof(double);
+        m.pbk = reinterpret_cast<double *>(p); p += (size_t)kSpcWaves * 64 * sizeof(double);
+        m.pbx = reinterpret_cast<int64_t *>(p); p += (size_t)kSpcWaves * 64 * sizeof(int64_t);
+        m.LK = reinterpret_cast<double *>(p); p += (size_t)K * 64 * sizeof(double);
+        m.T = reinterpret_cast<SpcSlot *>(p); p += (size_t)kSpcSlots * sizeof(SpcSlot);
+        m.hk = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
+        m.HP = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
+        m.tkc = reinterpret_cast<uint32_t *>(p); p += 64 * sizeof(uint32_t);
+        m.ti = reinterpret_cast<int32_t *>(p); p += kSpcSlots * sizeof(int32_t);
+        m.LI = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
+        m.fcg = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+        m.dfacc = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+        m.gn = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+        m.gq = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+        m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
+        m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
+        m.own = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
+        m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * 5 * sizeof(uint64_t);
+        m.D = reinterpret_cast<int8_t *>(p);
+    }
+    const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
+    // every wave: lane = pod j of the batch (lanes >= nb carry a zero request and are never read).
+    // Issued before the prologue so these global loads overlap the list loads instead of following
+    // them behind a barrier.
+    const bool pj = lane < nb;
+    const LanePods lp = pre ? *pre : load_lane_pods<LAB>(A.pods, p0, nb);
+    const int64_t rc = lp.rc, rm = lp.rm, rp = lp.rp;
+    const uint64_t sel = lp.sel;
+    // the batch's candidate lists: fc0 and cut flag per pod, and every thread's list entries -- only
+    // their (key, idx | valid) words, all loads in flight at once.  Lists that are ready at entry (the
+    // stream pipeline) are loaded before the table initialisation so their latency overlaps it; the
+    // persistent commit loads them after wait(), when the merges have published them.
+    constexpr int kHeadPer = (64 * K + kSpcThreads - 1) / kSpcThreads;
+    uint64_t w0[kHeadPer], w1[kHeadPer];
+    int64_t fc0v = 0;
+    int cut0 = 0;
+    auto load_lists = [&]() {
+        fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
+        cut0 = (wave == 0 && pj) ? (int32_t)(uint32_t)(load_i64<COH>(
+                                       reinterpret_cast<const int64_t *>(A.lists + (size_t)lane * K) + 6) >> 32) : 0;
+#pragma unroll
+        for (int u = 0; u < kHeadPer; ++u) {
+            const int e = tid + u * kSpcThreads;
+            w0[u] = 0; w1[u] = 0;  // valid = 0
+            if (e < 64 * K && e / K < nb) {
+                const uint64_t *w = reinterpret_cast<const uint64_t *>(A.lists + e);
+                if (COH) { w0[u] = ld_coh(w); w1[u] = ld_coh(w + 1); }
+                else { w0[u] = w[0]; w1[u] = w[1]; }
+            }
+        }
+    };
+    if constexpr (!COH) load_lists();
+
+    // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
+    if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
+    __syncthreads();
+    const int nin = COH ? L->xcount : A.xin->count;  // <= 64
+    for (int e = tid; e < nin; e += kSpcThreads) {
+        const XRec xi = COH ? L->xe[e] : A.xin->e[e];
+        SpcSlot &x = m.T[e];
+        x.idx = xi.idx; x.mine = 0;
+        for (int r = 0; r < 3; ++r) { x.s0[r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+        x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+        m.ti[e] = xi.idx;
+        const int h = spc_pos_insert(m.hk, xi.idx);
+        atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
+    }
+    __syncthreads();
+
+    const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+    const double y3 = recip(3.0);
+    double *Srow = m.S + (size_t)lane * kSpcRow;
+
+    // inherited slots: keys at the current state, predicate deltas, per-wave partial row bests
+    {
+        int dfl = 0;
+        double pk = -__builtin_inf();
+        int32_t pi = kNoIdx, ps = -1;
+        for (int t = wave; t < nin; t += kSpcWaves) {
+            const SpcSlot &x = m.T[t];
+            const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
+            const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
+            dfl += (int)f1 - (int)f0;
+            const double k = lane_key<PRIO, DOM, LAB, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
+                                                           y3, x.price);
+            Srow[t] = k;
+            const bool up = k != -__builtin_inf() && better(k, x.idx, pk, pi);
+            pk = up ? k : pk; pi = up ? x.idx : pi; ps = up ? t : ps;
+        }
+        m.pbk[wave * 64 + lane] = pk;
+        m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
+        if (dfl != 0) atomicAdd(&m.dfacc[lane], dfl);
+    }
+
+    // ---- prologue part 2: the candidate lists (hash positions of their entries) ----
+    if (dbg) t_pre = __builtin_amdgcn_s_memtime() - t_start;
+    if (!wait()) return false;  // a workgroup barrier when it waits
+    if (dbg) t_start = __builtin_amdgcn_s_memtime();
+    if constexpr (COH) load_lists();
+#pragma unroll
+    for (int u = 0; u < kHeadPer; ++u) {
+        const int e = tid + u * kSpcThreads;
+        if (e < 64 * K) {
+            const int j = e / K, q = e % K;
+            const bool v = (uint32_t)(w1[u] >> 32) != 0;
+            const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
+            const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
+            m.LK[q * 64 + j] = key;
+            m.LI[q * 64 + j] = idx;
+            m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
+        }
+    }
+    __syncthreads();
+
+    // ---- wave 0 state: lane j = pod j ----
+    int32_t fcc = 0;          // predicate count with the confirmed commits
+    double rbk = -__builtin_inf();  // best confirmed touched slot (key, node, slot)
+    int32_t rbi = kNoIdx, rbs = -1;
+    int cv = 0, cut = 0;      // list length, cut flag
+    int32_t my_idx = 0, my_feas = 0;
+    double my_score = 0.0;
+    int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
+    int nT = nin, done = nb, W = 64;
+    int64_t placed = 0, nrounds = 0, nfail = 0;
+    if (wave == 0) {
+        fcc = pj ? (int32_t)(fc0v + m.dfacc[lane]) : 0;
+        cut = cut0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) cv += m.LI[q * 64 + lane] != kNoIdx;  // valid entries form a prefix
+        for (int w = 0; w < kSpcWaves; ++w) {
+            const double k = m.pbk[w * 64 + lane];
+            const int64_t x = m.pbx[w * 64 + lane];
+            const int32_t xi = (int32_t)(uint32_t)x;
+            if (k != -__builtin_inf() && better(k, xi, rbk, rbi)) { rbk = k; rbi = xi; rbs = (int32_t)(x >> 32); }
+        }
+        if (lane == 0) { m.ctl[0] = 0; m.ctl[2] = 0; }
+    }
+
+    int c = 0;
+    const uint64_t t_pro = dbg ? __builtin_amdgcn_s_memtime() - t_start : 0;
+    for (;;) {
+        // ---- step 1 (wave 0): guesses for pods [c, cend) ----
+        if (dbg) t_mark = __builtin_amdgcn_s_memtime();
+        if (wave == 0) {
+            const int cend = (c + W < nb) ? c + W : nb;
+            // Guesses by fixpoint iteration, lane = pod: g_i = the first list entry of pod i that is neither
+            // confirmed-taken nor proposed by a pod < i (own[pos] < i) in the previous iteration.  Pod i's
+            // proposal is final once those of all pods < i are, so the fixpoint is reached after at most
+            // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
+            // the rule (99 %), it is reached after two.
+            const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
+            const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
+            int32_t pq = -1, ph = kSpcInvalid;  // current proposal (list position, table position)
+            for (int it = 0;; ++it) {
+                int32_t nq = -1, nh = kSpcInvalid;
+                if (act) {
+                    for (int qq = 0; qq < K; ++qq) {
+                        const int pos = m.HP[qq * 64 + lane];
+                        if (pos == kSpcInvalid) break;  // valid entries form a prefix
+                        const bool tk = (m.tkc[pos >> 5] >> (pos & 31)) & 1u;
+                        if (!tk && m.own[pos] >= lane) { nq = qq; nh = pos; break; }
+                    }
+                }
+                const bool changed = __ballot(act && nq != pq) != 0;
+                if (act && pq >= 0) m.own[ph] = 64;
+                lds_order();
+                pq = nq; ph = nh;
+                if (!changed && it > 0) break;
+                if (act && pq >= 0) atomicMin(&m.own[ph], lane);
+                lds_order();
+            }
+            const uint64_t gm = __ballot(act && pq >= 0);
+            if (lane >= c && lane < cend) {
+                my_g = act ? (pq >= 0 ? 0 : -1) : -2;
+                my_q = pq;
+                my_h = act && pq >= 0 ? ph : kSpcInvalid;
+                my_s = act && pq >= 0 ? nT + __popcll(gm & ((1ull << lane) - 1ull)) : -1;
+            }
+            const bool in = lane >= c && lane < cend;
+            if (in && my_g == 0) my_g = m.LI[my_q * 64 + lane];  // the guessed node
+            m.gn[lane] = in ? my_g : -2;
+            m.gq[lane] = my_q;
+            m.gs[lane] = my_s;
+            m.fcg[lane] = 0;
+            if (lane == 0) { m.ctl[0] = c; m.ctl[1] = cend; }
+        }
+        __syncthreads();
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s1 += t - t_mark; t_mark = t; }
+        const int rc0 = m.ctl[0], rce = m.ctl[1];
+        // ---- step 2 (all waves): evaluate the guessed commits in parallel ----
+        {
+            double pk = -__builtin_inf();
+            int32_t pi = kNoIdx, ps = -1;
+            // the guessed entries' snapshot state, staged in LDS by every thread at once (one memory latency
+            // for the round; the evaluation below then holds no per-pod arrays in registers)
+            for (int e = tid; e < 64 * 5; e += kSpcThreads) {
+                const int k = e / 5, w = e % 5;
+                if (k >= rc0 && k < rce && m.gn[k] >= 0) {
+                    const uint64_t *src = reinterpret_cast<const uint64_t *>(A.lists + (size_t)k * K + m.gq[k]) + 2 + w;
+                    m.GS[e] = COH ? ld_coh(src) : *src;
+                }
+            }
+            __syncthreads();
+            for (int k = rc0 + wave; k < rce; k += kSpcWaves) {
+                const int32_t g = __builtin_amdgcn_readfirstlane(m.gn[k]);
+                if (g < 0) continue;  // wave-uniform
+                const int s = __builtin_amdgcn_readfirstlane(m.gs[k]);
+                const int64_t a0 = (int64_t)m.GS[k * 5], a1 = (int64_t)m.GS[k * 5 + 1], a2 = (int64_t)m.GS[k * 5 + 2];
+                const uint64_t lab = m.GS[k * 5 + 3];
+                const float pr = __uint_as_float((uint32_t)m.GS[k * 5 + 4]);
+                // commit of pod k: used += request, ONE pod (anchor/predicate.go:99-102)
+                const int64_t n0 = wsub(a0, rl64(rc, k)), n1 = wsub(a1, rl64(rm, k)), n2 = wsub(a2, 1);
+                const bool fo = fits(rc, rm, rp, sel, a0, a1, a2, lab, LAB);
+                const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
+                const int d = (int)fn - (int)fo;
+                const double kv = lane_key<PRIO, DOM, LAB, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, y3, pr);
+                Srow[s] = kv;
+                m.D[k * 64 + lane] = (int8_t)d;
+                if (lane > k) {
+                    if (d != 0) atomicAdd(&m.fcg[lane], d);
+                    const bool up = kv != -__builtin_inf() && better(kv, g, pk, pi);
+                    pk = up ? kv : pk; pi = up ? g : pi; ps = up ? s : ps;
+                }
+                if (lane == 0) {
+                    SpcSlot &x = m.T[s];
+                    x.idx = g; x.mine = 1;
+                    x.s0[0] = a0; x.s0[1] = a1; x.s0[2] = a2;
+                    x.sb[0] = a0; x.sb[1] = a1; x.sb[2] = a2;  // untouched before this batch
+                    x.cur[0] = n0; x.cur[1] = n1; x.cur[2] = n2;
+                    x.labels = lab; x.price = pr; x.pad = 0;
+                    m.ti[s] = g;
+                }
+            }
+            m.pbk[wave * 64 + lane] = pk;
+            m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
+        }
+        __syncthreads();
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s2 += t - t_mark; t_mark = t; }
+        // ---- step 3 (wave 0): check, confirm the valid prefix, resolve the first failure ----
+        if (wave == 0) {
+            ++nrounds;
+            const int cend = rce;
+            // t* = best of the confirmed slots and of the guessed commits before this pod
+            double tk = rbk;
+            int32_t ti = rbi, ts = rbs;
+            for (int w = 0; w < kSpcWaves; ++w) {
+                const double k = m.pbk[w * 64 + lane];
+                const int64_t x = m.pbx[w * 64 + lane];
+                const int32_t xi = (int32_t)(uint32_t)x;
+                const bool up = k != -__builtin_inf() && better(k, xi, tk, ti);
+                tk = up ? k : tk; ti = up ? xi : ti; ts = up ? (int32_t)(x >> 32) : ts;
+            }
+            const bool has_t = ti != kNoIdx;
+            const int32_t fcj = fcc + m.fcg[lane];
+            // kind: 0 no placement, 1 the guess (first touch), 2 t*, 3 overflow, 4 guess unknown (re-probe)
+            int kind;
+            double uk = -__builtin_inf();
+            if (fcj == 0) {
+                kind = 0;
+            } else if (my_g >= 0) {
+                uk = m.LK[my_q * 64 + lane];
+                kind = (has_t && better(tk, ti, uk, my_g)) ? 2 : 1;
+            } else if (my_g == -2) {
+                kind = 4;  // predicted no fit, but a node fits: u* was never looked up
+            } else if (!cut) {
+                kind = has_t ? 2 : 0;
+            } else if (cv > 0) {
+                const double lk = m.LK[(cv - 1) * 64 + lane];
+                const int32_t lx = m.LI[(cv - 1) * 64 + lane];
+                kind = (has_t && better(tk, ti, lk, lx)) ? 2 : 3;
+            } else {
+                kind = 3;  // unreachable: a cut list keeps at least its cutoff entry
+            }
+            const bool guessed_commit = my_g >= 0;
+            const bool valid = (kind == 0 && !guessed_commit) || (kind == 1);
+            const bool inw = lane >= c && lane < cend;
+            const uint64_t bad = __ballot(inw && !valid);
+            const int f = bad ? (int)__builtin_ctzll(bad) : cend;
+            // confirm [c, f)
+            const bool conf = lane >= c && lane < f;
+            if (conf) {
+                my_idx = kind == 1 ? my_g : (fcj == 0 ? -1 : -2);
+                my_score = kind == 1 ? (PRIO == kPrioPrice ? 0.0 - uk : uk) : 0.0;
+                my_feas = fcj;
+                if (guessed_commit) atomicOr(&m.tkc[my_h >> 5], 1u << (my_h & 31));
+            }
+            placed += __popcll(__ballot(conf && kind == 1));
+            const int ncg = __popcll(__ballot(conf && guessed_commit));
+            nT += ncg;
+            if (f < nb) {
+                // bring the confirmed state of the pods still to come up to date with [c, f)
+                for (int k = c; k < f; ++k) {
+                    const int32_t g = __builtin_amdgcn_readlane(my_g, k);
+                    if (g < 0) continue;
+                    const int s = __builtin_amdgcn_readlane(my_s, k);
+                    const double v = Srow[s];
+                    fcc += m.D[k * 64 + lane];
+                    const bool up = v != -__builtin_inf() && better(v, g, rbk, rbi);
+                    rbk = up ? v : rbk; rbi = up ? g : rbi; rbs = up ? s : rbs;
+                }
+            }
+            if (f < cend) {
+                ++nfail;
+                // resolve pod f exactly (its inputs are exact: every pod before it is confirmed)
+                int kf = __builtin_amdgcn_readlane(kind, f);
+                const int32_t fcf = __builtin_amdgcn_readlane(fcj, f);
+                double wk = readlane_f64(tk, f);
+                int32_t wi = __builtin_amdgcn_readlane(ti, f);
+                int s = __builtin_amdgcn_readlane(ts, f);
+                int qf = -1;
+                if (kf == 4) {
+                    // first list entry of pod f not in T (guesses before f are confirmed, later ones void)
+                    const int cvf = __builtin_amdgcn_readlane(cv, f);
+                    bool free_ = false;
+                    int32_t e = kNoIdx;
+                    if (lane < cvf) {
+                        e = m.LI[lane * 64 + f];
+                        const int pos = m.HP[lane * 64 + f];
+                        free_ = !((m.tkc[pos >> 5] >> (pos & 31)) & 1u);
+                    }
+                    const uint64_t fm = __ballot(free_);
+                    const bool ht = wi != kNoIdx;
+                    if (fm) {
+                        qf = __builtin_ctzll(fm);
+                        const int32_t ue = __builtin_amdgcn_readlane(e, qf);
+                        const double ukf = m.LK[qf * 64 + f];
+                        if (ht && better(wk, wi, ukf, ue)) kf = 2;
+                        else { kf = 1; wk = ukf; wi = ue; }
+                    } else if (!__builtin_amdgcn_readlane(cut, f)) {
+                        kf = ht ? 2 : 0;
+                    } else if (cvf > 0) {
+                        const double lk = m.LK[(cvf - 1) * 64 + f];
+                        const int32_t lx = m.LI[(cvf - 1) * 64 + f];
+                        kf = (ht && better(wk, wi, lk, lx)) ? 2 : 3;
+                    } else {
+                        kf = 3;
+                    }
+                }
+                kf = __builtin_amdgcn_readfirstlane(kf);
+                if (kf == 3) {
+                    done = f;  // overflow: the batch stops before pod f
+                } else {
+                    if (lane == f) {
+                        my_idx = kf == 0 ? (fcf == 0 ? -1 : -2) : wi;
+                        my_score = kf == 0 ? 0.0 : (PRIO == kPrioPrice ? 0.0 - wk : wk);
+                        my_feas = fcf;
+                    }
+                    if (kf != 0) {
+                        ++placed;
+                        int64_t b0, b1, b2;
+                        uint64_t lab;
+                        float pr;
+                        if (kf == 1) {  // first touch of list entry qf
+                            int64_t ra[3];
+                            load_rec_state<COH>(A.lists + (size_t)f * K + qf, ra, &lab, &pr);
+                            b0 = ra[0]; b1 = ra[1]; b2 = ra[2];
+                            s = nT++;
+                        } else {
+                            const SpcSlot &x = m.T[s];
+                            b0 = x.cur[0]; b1 = x.cur[1]; b2 = x.cur[2]; lab = x.labels; pr = x.price;
+                        }
+                        const int64_t n0 = wsub(b0, rl64(rc, f)), n1 = wsub(b1, rl64(rm, f)), n2 = wsub(b2, 1);
+                        const bool fo = fits(rc, rm, rp, sel, b0, b1, b2, lab, LAB);
+                        const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
+                        fcc += (int32_t)fn - (int32_t)fo;
+                        const double kv =
+                            lane_key<PRIO, DOM, LAB, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, y3, pr);
+                        Srow[s] = kv;
+                        if (lane == 0) {
+                            SpcSlot &x = m.T[s];
+                            if (kf == 1) {
+                                x.idx = wi;
+                                x.s0[0] = b0; x.s0[1] = b1; x.s0[2] = b2;
+                                x.sb[0] = b0; x.sb[1] = b1; x.sb[2] = b2;
+                                x.labels = lab; x.price = pr; x.pad = 0;
+                                m.ti[s] = wi;
+                                const int pos = m.HP[qf * 64 + f];
+                                m.tkc[pos >> 5] |= 1u << (pos & 31);
+                            }
+                            x.mine = 1;
+                            x.cur[0] = n0; x.cur[1] = n1; x.cur[2] = n2;
+                        }
+                        lds_order();
+                        // running best: a better value takes over; a holder that got worse forces a rescan
+                        const bool up = kv != -__builtin_inf() && better(kv, wi, rbk, rbi);
+                        const bool rescan = !up && rbs == s;
+                        rbk = up ? kv : rbk; rbi = up ? wi : rbi; rbs = up ? s : rbs;
+                        if (__ballot(rescan)) {
+                            if (rescan) {
+                                rbk = -__builtin_inf(); rbi = kNoIdx; rbs = -1;
+                                for (int t = 0; t < nT; ++t) {
+                                    const double v = Srow[t];
+                                    const int32_t x = m.ti[t];
+                                    if (v != -__builtin_inf() && better(v, x, rbk, rbi)) { rbk = v; rbi = x; rbs = t; }
+                                }
+                            }
+                        }
+                    }
+                }
+                W = 2 * (f - c + 1);
+                W = W < 4 ? 4 : (W > 64 ? 64 : W);
+                c = f + 1;
+            } else {
+                W = 2 * W > 64 ? 64 : 2 * W;
+                c = cend;
+            }
+            if (lane == 0) { m.ctl[0] = c; m.ctl[2] = (done < nb || c >= nb) ? 1 : 0; }
+        }
+        __syncthreads();
+        if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s3 += t - t_mark; t_mark = t; }
+        if (m.ctl[2]) break;
+        c = m.ctl[0];
+    }
+    if (wave != 0) return true;
+
+    if (lane < done) {
+        A.out.idx[p0 + lane] = my_idx;
+        A.out.score[p0 + lane] = my_score;
+        A.out.feas[p0 + lane] = my_feas;
+    }
+    // export this batch's commits (wave-ordered compaction)
+    int base = 0;
+    for (int t0 = 0; t0 < nT; t0 += 64) {
+        const int t = t0 + lane;
+        const bool mine = t < nT && m.T[t].mine;
+        const uint64_t mask = __ballot(mine);
+        if (mine) {
+            const SpcSlot &x = m.T[t];
+            XRec o;
+            o.idx = x.idx; o.pad = 0;
+            o.sb[0] = x.sb[0]; o.sb[1] = x.sb[1]; o.sb[2] = x.sb[2];
+            o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
+            o.labels = x.labels; o.price = x.price; o.pad2 = 0;
+            const int slot = base + __popcll(mask & ((1ull << lane) - 1));
+            store_xrec<COH>(&A.xout->e[slot], o);
+            if (COH) L->xe[slot] = o;  // the next batch inherits it from LDS (every inherited read is done)
+        }
+        base += __popcll(mask);
+    }
+    if (lane == 0) {
+        if (COH) {
+            st_coh(&A.xout->count, (uint64_t)(uint32_t)base);
+            L->xcount = base;
+            L->cursor = p0 + done;
+            st_coh(&A.ctl->cursor, (uint64_t)(p0 + done));
+            L->stats[0] += 1;
+            L->stats[1] += (done < nb) ? 1 : 0;
+            L->stats[2] += placed;
+            for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
+            persist_plan(A, done < nb, p0 + done);
+        } else {
+            A.xout->count = base;
+            store_i64<COH>(&A.ctl->cursor, p0 + done);
+            add_i64<COH>(&A.ctl->stats[0], 1);
+            add_i64<COH>(&A.ctl->stats[1], (done < nb) ? 1 : 0);
+            add_i64<COH>(&A.ctl->stats[2], placed);
+            plan_after_commit<COH>(A, done < nb, p0 + done);
+        }
+        if (A.dbg) {
+            A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1;
+            A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
+            A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
+            A.dbg[6] += t_pre;
+        }
+    }
+    publish_committed<COH>(A);  // wave 0 made every global store of this batch
+    return true;
+}
+
+template <int K, int NT = kSpcThreads>
+constexpr size_t spc_lds_bytes() {
+    return (size_t)64 * kSpcRow * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 + kSpcSlots * sizeof(SpcSlot) +
+           (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 + kSpcSlots * 4 + 5 * 64 * 4 + 16 + (size_t)kSpcHash * 4 +
+           64 * 5 * 8 + 64 * 64;
+}
+static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
+
+}  // namespace ksched

@@ -89,7 +89,6 @@ struct ksched_ctx {
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
     int64_t *d_mdbg = nullptr;    // KSCHED_MERGE_STAMPS diagnostics
     hipStream_t stream2 = nullptr;  // merge + commit stream of the batched pipeline
-    hipStream_t stream3 = nullptr;  // persistent pipeline: the merger workgroups' stream (created on first use)
     hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[3] = {};
     void *d_xring = nullptr, *d_lring = nullptr;
     int64_t xring_bytes = 0, lring_bytes = 0;
@@ -133,6 +132,16 @@ struct ksched_ctx {
     bool xchg_run = false;         // the current run uses the exchange
     uint32_t xchg_epoch = 1;       // granule tag base of the next call (identical on every rank)
     int32_t *d_xmin = nullptr;     // k_xchg_min result
+    // diagnostics, read from the environment once at ksched_create (never a tuning switch):
+    //   KSCHED_PERSIST_TRACE=1   per-batch phase stamps of the persistent pipeline, summary to stderr at sync
+    //   KSCHED_COMMIT_STAMPS=1   commit phase cycle sums;  KSCHED_MERGE_STAMPS=1  merge phase cycle sums
+    //   KSCHED_PERSIST_TIMEOUT_MS (10000)  bound of every persistent-pipeline wait (tests force timeouts with 0)
+    //   KSCHED_EXCHANGE_TIMEOUT_MS (2000)  bound of the exact kernel's cross-workgroup exchange
+    //   KSCHED_DEBUG=1           launch decisions to stderr
+    struct {
+        bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
+        int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
+    } diag;
 };
 
 namespace {
@@ -223,10 +232,10 @@ BatchPlan plan_batch(const ksched_ctx *c) {
     pl.pod_groups = (pl.B + 63) / 64;
     const int64_t n = std::max<int64_t>(c->n_local, 1);
     // NSC sub-chunks (one wave each) in workgroups of kScoreWaves: 8 waves per CU at full size,
-    // >= KSCHED_MIN_CHUNK nodes per wave, <= kMergeThreads workgroups (one merge lane per list)
-    const int target_waves = env_int("KSCHED_TARGET_WAVES", c->cus * 8);
+    // >= 16 nodes per wave, <= kMergeThreads workgroups (one merge lane per list)
+    const int target_waves = c->cus * 8;
     int64_t nsc = std::max<int64_t>(1, target_waves / pl.pod_groups);
-    const int min_s = env_int("KSCHED_MIN_CHUNK", 16);
+    const int min_s = 16;
     nsc = std::min<int64_t>(nsc, (n + min_s - 1) / min_s);
     nsc = std::min<int64_t>(nsc, (int64_t)kMergeThreads * kScoreWaves);
     nsc = std::max<int64_t>(kScoreWaves, nsc / kScoreWaves * kScoreWaves);
@@ -267,7 +276,6 @@ void fill_xchg_args(const ksched_ctx *c, PersistArgs *a) {
 // fast53 for this call: every |alloc| + sum of |requests| < 2^52, on every rank.
 int decide_fast53(ksched_ctx *c) {
     int flag = sat_add(c->max_abs_alloc, c->sum_abs_req) < (1ull << 52) ? 1 : 0;
-    if (env_int("KSCHED_NO_FAST53", 0)) flag = 0;
     if (c->group) {
         int mn = flag;
         if (!group_min(c->group, flag, &mn)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer never called run");
@@ -277,7 +285,7 @@ int decide_fast53(ksched_ctx *c) {
         PersistArgs a{};
         fill_xchg_args(c, &a);
         a.err = c->d_err;
-        a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
+        a.timeout_ticks = c->diag.persist_timeout_ms * 100000;
         int32_t mn = -1;
         HIPCHK(c, launch_xchg_min(a, flag, c->d_xmin, c->stream));
         HIPCHK(c, hipMemcpyAsync(&mn, c->d_xmin, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -310,8 +318,8 @@ int decide_fast53(ksched_ctx *c) {
 // speculation, which commit skips, and plans its restart at the committed frontier.
 // The commit(b-2) -> score(b) edge is a device-side flag (score(b) is already resident when it is
 // released: ~2 us) instead of a cross-queue stream event (~13 us per batch measured on MI355X, even
-// when the event has completed: profiles/r02_*).  score(b) -> merge(b) stays an event unless the merge
-// polls Ctl::scored (KSCHED_DEVICE_HANDOFF=1).
+// when the event has completed: profiles/r02_*) wherever the commit provably fits beside a resident
+// score workgroup; score(b) -> merge(b) is a stream event.
 int enqueue_batched(ksched_ctx *c) {
     const BatchPlan pl = plan_batch(c);
     if (c->ws_bytes < (int64_t)pl.total) {
@@ -336,10 +344,7 @@ int enqueue_batched(ksched_ctx *c) {
     const bool spc_commit = impl != KSCHED_COMMIT_SEQUENTIAL;
     hipStream_t sS = c->stream, sC = c->stream2;
     // device-side score wait only where the commit provably fits beside a resident score workgroup
-    const bool score_poll = env_int("KSCHED_SCORE_EVENT", 0) == 0 &&
-                            commit_fits_beside_score(pl.KC, pl.K, pl.B, spc_commit, prio, dom, lab, f53);
-    const bool dev_handoff = env_int("KSCHED_DEVICE_HANDOFF", 0) != 0;
-    unsigned long long scored_target = 0;
+    const bool score_poll = commit_fits_beside_score(pl.KC, pl.K, pl.B, spc_commit, prio, dom, lab, f53);
     constexpr int kRing = 4;  // lists / X buffers / events in flight
     const size_t xb = xbuf_bytes(pl.B);
     if (c->xring_bytes < (int64_t)(xb * (kRing + 1))) {
@@ -361,9 +366,9 @@ int enqueue_batched(ksched_ctx *c) {
     Ctl *ctl = reinterpret_cast<Ctl *>(c->d_cursor);
     HIPCHK(c, launch_ctl_init(ctl, pl.B, c->p, sS));
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
-    if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
+    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
-    if (env_int("KSCHED_MERGE_STAMPS", 0) && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
+    if (c->diag.merge_stamps && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
     if (c->d_mdbg) HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), sS));
     HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // stream C starts after the initialisation above
     HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
@@ -393,15 +398,11 @@ int enqueue_batched(ksched_ctx *c) {
             sa.part = reinterpret_cast<Cand *>(ws + pl.off_part) + (size_t)(b % 2) * part_elems * pl.KC;
             sa.part_cnt = reinterpret_cast<int64_t *>(ws + pl.off_pcnt) + (size_t)(b % 2) * part_elems;
             sa.patch = xbuf(b - 2);
-            sa.done = dev_handoff ? &ctl->scored : nullptr;
-            scored_target += (unsigned long long)(pl.n_chunks / kScoreWaves) * (unsigned long long)pl.pod_groups;
             MergeArgs ma{};
             ma.in = sa.part; ma.in_cnt = sa.part_cnt; ma.C_in = pl.C[0]; ma.C_out = 1; ma.chunk_input = 1;
             ma.cursor = plan; ma.P = c->p; ma.B = pl.B;
             ma.nodes = c->d_nodes; ma.node_offset = c->o.node_offset;
             ma.dbg = c->d_mdbg;
-            ma.wait_ctr = dev_handoff ? &ctl->scored : nullptr;
-            ma.wait_target = scored_target;
             ma.err = c->d_err;
             ma.out_rec = reinterpret_cast<Rec *>(lists_base);
             ma.out_fc = reinterpret_cast<int64_t *>(lists_base + (size_t)pl.B * pl.K * sizeof(Rec));
@@ -409,10 +410,8 @@ int enqueue_batched(ksched_ctx *c) {
             HIPCHK(c, launch_score_topk(pl.KC, prio, dom, lab, f53, sa, pl.pod_groups, sS));
             HIPCHK(c, ev_end(c, tm, 0, e0, (int64_t)pl.B * c->n_local, sS));
             // C: merge b while stream S scores b+1 (the lists' part buffers alternate)
-            if (!dev_handoff) {
-                HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
-                HIPCHK(c, hipStreamWaitEvent(sC, c->ev_scored[b % kRing], 0));
-            }
+            HIPCHK(c, hipEventRecord(c->ev_scored[b % kRing], sS));
+            HIPCHK(c, hipStreamWaitEvent(sC, c->ev_scored[b % kRing], 0));
             HIPCHK(c, ev_begin(c, tm, &e0, sC));
             HIPCHK(c, launch_merge_pod(pl.KC, pl.K, ma, sC));
             HIPCHK(c, ev_end(c, tm, 1, e0, 0, sC));
@@ -509,10 +508,6 @@ int enqueue_batched(ksched_ctx *c) {
     return KSCHED_OK;
 }
 
-// Single-rank batched mode as two resident kernels (ksched_persist.hip): no per-batch launches, no
-// stream events, node rows in LDS.  Returns 1 (not taken) when the configuration does not fit it --
-// multi-rank, a sequential commit (batch > 64), chunk lists > 8, or rows that do not fit in LDS --
-// and the stream pipeline runs instead.
 // KSCHED_PERSIST_TRACE=1: mean per-batch phase times of the last persistent run, to stderr (us)
 void print_persist_trace(ksched_ctx *c) {
     std::vector<uint64_t> t((size_t)c->trace_cap * kTraceCols);
@@ -568,32 +563,42 @@ void print_persist_trace(ksched_ctx *c) {
             sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
 }
 
-constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
-
+// Batched mode as ONE persistent kernel (ksched_pipe.hip): no per-batch launches, no stream events,
+// node rows in LDS.  Returns 1 (not taken) when the configuration does not fit it -- the stream pipeline
+// was asked for, multi-rank without the device exchange, a sequential commit (batch > 64), chunk lists
+// other than 4 / 8, more lists than merge threads, or rows that do not fit in LDS -- and the stream
+// pipeline runs instead.
 int enqueue_persistent(ksched_ctx *c) {
-    if (env_int("KSCHED_PERSIST", 1) == 0) return 1;
+    if (c->o.pipeline == KSCHED_PIPELINE_STREAM) return 1;
     // single rank, or node-sharded with the device-side exchange (the RCCL / in-process group paths
     // run the stream pipeline)
     if (!c->xchg_run && (c->comm || c->group || c->o.nranks > 1 || c->o.node_offset != 0)) return 1;
     const int K = c->K, KC = c->KC, B = c->B;
-    if (B > 64 || KC > 8 || (c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL)) return 1;
+    if (B > 64 || (KC != 4 && KC != 8) || (c->o.commit_impl == KSCHED_COMMIT_SEQUENTIAL)) return 1;
     const int64_t n = c->n_local;
     // node-sharded: every rank sizes its grid for the largest shard, so all ranks take the same path
     const int64_t n_geom = c->xchg_run ? std::max<int64_t>(n, (c->n_global + c->o.nranks - 1) / c->o.nranks) : n;
-    // workgroups of a launch go round-robin to the 8 XCDs (32 CUs each), so the grid must leave one CU
-    // free on EVERY XCD for the commit workgroup to be guaranteed a place: G <= CUs - 8 (measured: with
-    // G = CUs - 2 one score workgroup of the XCD the commit sits on never starts).  The default leaves TWO
-    // per XCD: at G = CUs - 8 the commit's XCD is full, and in about one c4 call in twenty the last two score
-    // workgroups dispatched to it stalled inside their export apply for seconds (per-wave marks, DESIGN.md
-    // section 4.1); at CUs - 16 none did in 60 calls (c4 1.61e11 -> 1.56e11 evals/s).
-    const int gcap = (int)std::min<int64_t>(c->cus - kXcds, env_int("KSCHED_PERSIST_G", c->cus - 2 * kXcds));
-    // at least ~96 rows per workgroup: a smaller grid costs scan time but every list fewer shortens the merge
-    // (one rank's share of an 8-GPU c4, 12.5k nodes: G = 128 -> 22.8 us per batch, 240 -> 23.8, 64 -> 24.6)
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>(gcap, (n_geom + 95) / 96));
-    if (G > c->cus - kXcds) return 1;
+    // one workgroup per CU: the commit + G score workgroups.  At least ~96 rows per workgroup: a smaller
+    // grid costs scan time but every list fewer shortens the merge (one rank's share of an 8-GPU c4,
+    // 12.5k nodes: G = 128 -> 22.8 us per batch, 240 -> 23.8, 64 -> 24.6; round 2)
+    const int wgs = c->o.pipe_wgs > 0 ? std::min(c->o.pipe_wgs, c->cus) : c->cus;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1, (int64_t)kPipeMergeThreads,
+                                                               (n_geom + 95) / 96}));
+    if (wgs < 2) return 1;
     const int R = (int)((n_geom + G - 1) / G);
-    const size_t lds = persist_score_lds(KC, R);
-    if (lds == 0) return 1;
+    PersistArgs a{};
+    a.rows_per_wg = R;
+    a.G = G;
+    a.B = B;
+    PipeInfo info{};
+    const bool f53 = c->fast53, lab = c->o.use_labels != 0;
+    hipError_t e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, a, 0, &info, c->stream);
+    if (e == hipErrorNotSupported) return 1;
+    HIPCHK(c, e);
+    if (c->diag.debug)
+        fprintf(stderr, "[ksched pipe] G=%d rows/wg=%d LDS %zu+%zu B, %d VGPRs, %zu B scratch\n", G, R, info.lds,
+                info.static_lds, info.vgprs, info.spill);
+    if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
     // workspace: part lists [2][B][G][KC] + counts [2][B][G], list ring 4 x (B*K Rec + B fc), XBuf ring
     const size_t part_b = align_up((size_t)2 * B * G * KC * sizeof(Cand), 256);
     const size_t cnt_b = align_up((size_t)2 * B * G * sizeof(int64_t), 256);
@@ -603,9 +608,6 @@ int enqueue_persistent(ksched_ctx *c) {
     const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b;
     if (c->pws_bytes < need) {
         if (c->d_pws) hipFree(c->d_pws);
-        if (c->d_trace) hipFree(c->d_trace);
-        c->d_trace = nullptr;
-        c->trace_cap = 0;
         c->d_pws = nullptr;
         c->d_prog = nullptr;
         c->pws_bytes = 0;
@@ -613,11 +615,9 @@ int enqueue_persistent(ksched_ctx *c) {
         c->pws_bytes = need;
     }
     char *w = static_cast<char *>(c->d_pws);
-    PersistArgs a{};
     a.nodes = c->d_nodes; a.n_local = n;
     a.pods = PodArgs{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
     a.ctl = reinterpret_cast<Ctl *>(c->d_cursor);
-    a.B = B; a.G = G; a.rows_per_wg = R;
     a.part = reinterpret_cast<Cand *>(w);
     a.part_cnt = reinterpret_cast<int64_t *>(w + part_b);
     a.lring = w + part_b + cnt_b;
@@ -630,14 +630,11 @@ int enqueue_persistent(ksched_ctx *c) {
     c->prog_B = B;
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     fill_xchg_args(c, &a);
-    a.merge_low_prio = env_int("KSCHED_MERGE_LOW_PRIO", 0);
-    a.prog_waves = env_int("KSCHED_PROG_WAVES", 0);
-    a.commit_release = env_int("KSCHED_COMMIT_RELEASE", 0);
     a.err = c->d_err;
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)
-    a.timeout_ticks = (int64_t)env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000) * 100000;
-    if (env_int("KSCHED_PERSIST_TRACE", 0)) {
+    a.timeout_ticks = c->diag.persist_timeout_ms * 100000;
+    if (c->diag.trace) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {
             if (c->d_trace) hipFree(c->d_trace);
@@ -650,42 +647,38 @@ int enqueue_persistent(ksched_ctx *c) {
         a.trace = c->d_trace;
         a.trace_cap = c->trace_cap;
     }
-    if (env_int("KSCHED_COMMIT_STAMPS", 0) && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
+    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) {
         HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), c->stream));
         a.cdbg = c->d_dbg;
     }
-    if (env_int("KSCHED_MERGE_STAMPS", 0) && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
+    if (c->diag.merge_stamps && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
     if (c->d_mdbg) {
         HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), c->stream));
         a.mdbg = c->d_mdbg;
     }
-    if (!c->stream3) HIPCHK(c, hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking));
-    hipStream_t sS = c->stream, sC = c->stream2, sM = c->stream3;
+    hipStream_t sS = c->stream;
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
     HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + 1) * kProgWords * 8, sS));
-    HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // the commit and merge streams start after the initialisation
-    HIPCHK(c, hipStreamWaitEvent(sC, c->ev_pipe[0], 0));
-    HIPCHK(c, hipStreamWaitEvent(sM, c->ev_pipe[0], 0));
-    // timing: the score grid's launch (family 0) is bracketed by events on ITS stream -- one launch per
-    // call, so the events cost nothing per batch and may stay on inside a timed region
+    // timing: the kernel (family 0) is bracketed by events on its stream -- one launch per call, so the
+    // events cost nothing per batch and may stay on inside a timed region
     int e0 = -1;
     HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, sS));
-    const hipError_t e =
-        launch_persist(KC, K, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, lds, sS, sC, sM);
-    if (e == hipErrorInvalidValue) {  // does not fit after all: the stream pipeline runs
-        if (env_int("KSCHED_DEBUG", 0)) fprintf(stderr, "[ksched persist] launch_persist: does not fit\n");
+    // cooperative launch: the runtime checks the grid against the occupancy query, so every workgroup is
+    // resident at once.  Ranks sharing one device (pipe_wgs) launch plainly: each takes a share of the CUs
+    // and the cooperative launch would serialise them.
+    const int how = c->o.pipe_wgs > 0 ? 2 : 1;
+    e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, a, how, nullptr, sS);
+    if (e == hipErrorCooperativeLaunchTooLarge && !c->xchg_run) {  // the stream pipeline runs instead
+        if (c->diag.debug) fprintf(stderr, "[ksched pipe] cooperative launch too large: stream pipeline\n");
+        (void)hipGetLastError();
         c->timed.clear();
         c->ev_used = 0;
         return 1;
     }
-    if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("launch_persist: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return fail(c, KSCHED_E_DEVICE, std::string("launch_pipe: ") + hipGetErrorString(e));
     HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n, sS));
-    HIPCHK(c, hipEventRecord(c->ev_pipe[1], sC));  // the run's end event on stream S covers commit + merge
-    HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[1], 0));
-    HIPCHK(c, hipEventRecord(c->ev_pipe[2], sM));
-    HIPCHK(c, hipStreamWaitEvent(sS, c->ev_pipe[2], 0));
     HIPCHK(c, hipMemcpyAsync(c->h_cursor, a.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, sS));
     c->persist_stats = true;
     c->persist_B = B;
@@ -696,7 +689,7 @@ int enqueue_persistent(ksched_ctx *c) {
 int enqueue_exact(ksched_ctx *c) {
     if (c->o.nranks > 1) return fail(c, KSCHED_E_INVALID, "exact mode is single-GPU; use batched mode across ranks");
     const int64_t n = c->n_local;
-    int G = c->o.exact_wgs > 0 ? c->o.exact_wgs : env_int("KSCHED_EXACT_WGS", 0);
+    int G = c->o.exact_wgs;
     int npt;
     if (G <= 0) {
         // resource scores are ~150 FP64 ops per pair: spread nodes thin; best-price is a compare: pack
@@ -721,7 +714,7 @@ int enqueue_exact(ksched_ctx *c) {
     a.pods = PodArgs{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     a.slots = c->d_slots; a.err = c->d_err;
-    a.timeout_ticks = (int64_t)env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000) * 100000;  // 100 MHz wall clock
+    a.timeout_ticks = c->diag.exchange_timeout_ms * 100000;  // 100 MHz wall clock
     int e0 = -1;
     HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, c->stream));
     HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, kExactBlock, G > 1,
@@ -765,10 +758,17 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->K = opts->topk ? opts->topk : 16;
     if (opts->chunk_topk != 0 && opts->chunk_topk != 2 && opts->chunk_topk != 4 && opts->chunk_topk != 8 &&
         opts->chunk_topk != 16) { delete c; return KSCHED_E_INVALID; }
-    c->KC = std::min(c->K, opts->chunk_topk ? opts->chunk_topk : env_int("KSCHED_CHUNK_TOPK", 4));
+    c->KC = std::min(c->K, opts->chunk_topk ? opts->chunk_topk : 4);
     c->B = opts->batch > 0 ? opts->batch : std::min(128, 8 * c->K);
     if (c->B > 128) { delete c; return KSCHED_E_INVALID; }
     if (opts->commit_impl < 0 || opts->commit_impl > 3) { delete c; return KSCHED_E_INVALID; }
+    if (opts->pipeline < 0 || opts->pipeline > 1 || opts->pipe_wgs < 0) { delete c; return KSCHED_E_INVALID; }
+    c->diag.trace = env_int("KSCHED_PERSIST_TRACE", 0) != 0;
+    c->diag.commit_stamps = env_int("KSCHED_COMMIT_STAMPS", 0) != 0;
+    c->diag.merge_stamps = env_int("KSCHED_MERGE_STAMPS", 0) != 0;
+    c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
+    c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
+    c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) { delete c; return KSCHED_E_DEVICE; }
@@ -808,7 +808,6 @@ int ksched_destroy(ksched_ctx *c) {
     hipSetDevice(c->dev);
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->stream2) hipStreamSynchronize(c->stream2);
-    if (c->stream3) hipStreamSynchronize(c->stream3);
     if (c->comm) ncclCommDestroy(c->comm);
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
@@ -831,7 +830,6 @@ int ksched_destroy(ksched_ctx *c) {
     hipFree(c->d_rx);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
-    if (c->stream3) hipStreamDestroy(c->stream3);
     delete c;
     return KSCHED_OK;
 }
@@ -941,6 +939,13 @@ int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
 }
 
 int ksched_xchg_ready(const ksched_ctx *c) { return c && c->xchg_ready ? 1 : 0; }
+
+int ksched_xchg_close(ksched_ctx *c) {
+    if (!c) return KSCHED_E_INVALID;
+    c->xchg_ready = false;
+    c->xchg_run = false;
+    return KSCHED_OK;
+}
 
 int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t *am, const int64_t *ap,
                       const uint64_t *labels, const float *price) {
@@ -1228,7 +1233,11 @@ int ksched_run(ksched_ctx *c) {
     c->st.pods = c->p;
     int mode = c->o.mode;
     if (mode == KSCHED_MODE_AUTO) mode = c->o.nranks > 1 ? KSCHED_MODE_BATCHED : KSCHED_MODE_EXACT;
-    c->xchg_run = c->xchg_ready && mode == KSCHED_MODE_BATCHED && c->p > 0 && env_int("KSCHED_XCHG", 1) != 0;
+    c->xchg_run = c->xchg_ready && mode == KSCHED_MODE_BATCHED && c->p > 0;
+    // a multi-rank batched call needs a transport: the device exchange, an RCCL communicator or a rank group
+    // (never a rank committing from its own shard alone)
+    if (c->o.nranks > 1 && mode == KSCHED_MODE_BATCHED && c->p > 0 && !c->xchg_run && !c->comm && !c->group)
+        return fail(c, KSCHED_E_STATE, "run: multi-rank context without an exchange transport");
     if (int rr = decide_fast53(c)) return rr;
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     int r = KSCHED_OK;
@@ -1347,8 +1356,18 @@ static std::string progress_summary(ksched_ctx *c) {
     return out;
 }
 
+static int sync_impl(ksched_ctx *c);
+
 int ksched_sync(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
+    const int r = sync_impl(c);
+    // a failed call left the node state partly committed: no FailedScheduling replay from it (callers
+    // restore_state / load_nodes before retrying)
+    if (r != KSCHED_OK) c->explain_valid = false;
+    return r;
+}
+
+static int sync_impl(ksched_ctx *c) {
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->running) {
@@ -1365,7 +1384,7 @@ int ksched_sync(ksched_ctx *c) {
         }
         c->timed.clear();
     }
-    if (c->persist_stats && c->d_trace && env_int("KSCHED_PERSIST_TRACE", 0)) {
+    if (c->persist_stats && c->d_trace && c->diag.trace) {
         print_persist_trace(c);
         print_wg_busy(c);
     }
@@ -1432,6 +1451,12 @@ int ksched_download_results(ksched_ctx *c, int64_t p, int32_t *oi, double *os, i
 int ksched_get_stats(const ksched_ctx *c, ksched_stats *out) {
     if (!c || !out) return KSCHED_E_INVALID;
     *out = c->st;
+    return KSCHED_OK;
+}
+
+int ksched_set_timeout(ksched_ctx *c, int32_t persist_ms) {
+    if (!c || persist_ms < 0) return KSCHED_E_INVALID;
+    c->diag.persist_timeout_ms = persist_ms;
     return KSCHED_OK;
 }
 

@@ -150,7 +150,6 @@ struct ScoreArgs {
     Cand *part;        // [B][workgroups][KC]
     int64_t *part_cnt; // [B][workgroups]
     const XBuf *patch; // batch b-2's commits: overlaid on the rows as they are read, then written back
-    unsigned long long *done;  // Ctl::scored (null: the merge waits on a stream event instead)
     // device-side wait for commit(b-2): poll *wait_committed >= wait_target (null: the stream waits)
     const unsigned long long *wait_committed;
     unsigned long long wait_target;
@@ -177,11 +176,8 @@ struct MergeArgs {
     int32_t B;
     int32_t p0_known;   // 1: p0v is this batch's first pod (the persistent score grid read it already)
     int64_t p0v;
-    const unsigned long long *wait_ctr;  // k_merge_pod: poll until *wait_ctr >= wait_target (null: no wait)
-    unsigned long long wait_target;
-    int32_t *err;                        // device error word (2 = the wait timed out)
+    int32_t *err;                        // device error word
     uint32_t *lds_msg;                   // non-null: the final list goes to LDS as a PodMsg (kMsgWords)
-    int32_t low_prio;                    // 1: merge waves at issue priority 0 (persistent mergers, A/B)
 };
 
 // One pod's merged candidate list as 32-bit words, the unit the ranks exchange in the persistent
@@ -375,16 +371,13 @@ struct PersistArgs {
     uint32_t epoch0;        // granule tag of this call's active batch a is epoch0 + a (a >= 1)
     int64_t xchg_stride;    // bytes per pod message in a ring
     char *rx_peer[8];       // every rank's receive ring, mapped into this process (rx_peer[rank] = own)
-    int32_t merge_low_prio; // KSCHED_MERGE_LOW_PRIO: mergers yield issue slots to the score waves
     // progress words, kProgWords per workgroup ([G] score, [B] merger, [1] commit): {batch << 8 | phase, hw id
     // << 32 | low word of the last value a wait saw, busy-time sums}; read by the host when a wait timed out
     // (and by the phase trace)
     uint64_t *prog;
-    int32_t prog_waves;     // KSCHED_PROG_WAVES: every score wave marks its position (prog words 4..11)
-    int32_t commit_release; // KSCHED_COMMIT_RELEASE: agent release (L2 write-back) before each publication
 };
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
-constexpr int kProgWords = 12;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4..11 per-wave marks
+constexpr int kProgWords = 4;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy
 enum : int { kProgWaitCommit = 1, kProgScan = 2, kProgArrived = 3, kProgWaitArrive = 4, kProgMerged = 5,
              kProgWaitMerged = 6, kProgCommitted = 7, kProgIdle = 8, kProgTimedOut = 0x80 };
 __device__ __forceinline__ uint32_t hw_where() {
@@ -400,12 +393,6 @@ __device__ __forceinline__ void prog_at(const PersistArgs &P, int slot, int64_t 
                        __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(P.prog + kProgWords * slot + 1, (uint64_t)hw_where() << 32 | (seen & 0xffffffffull),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// score wave `wave` of workgroup `slot` reached mark `code` of batch b (lane 0; KSCHED_PROG_WAVES only)
-__device__ __forceinline__ void wave_mark(const PersistArgs &P, int slot, int wave, int64_t b, int code) {
-    if (!P.prog_waves || (threadIdx.x & 63) != 0) return;
-    __hip_atomic_store(P.prog + kProgWords * slot + 4 + wave, (uint64_t)b << 8 | (uint64_t)code, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
 }
 // busy-time sums of a workgroup (KSCHED_PERSIST_TRACE calls only: P.trace set): word 2 += scan ticks, word 3
 // += ticks from its wait's end to its arrival (word 2 is the heartbeat of a long wait otherwise)
@@ -461,11 +448,33 @@ constexpr int kTraceCols = 16;
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }
-hipError_t launch_persist_commit(int K, int prio, int dom, bool lab, bool fast53, const PersistArgs &a, hipStream_t s);
-// bytes of dynamic LDS the score grid needs (0: the rows do not fit -> use the stream pipeline)
-size_t persist_score_lds(int KC, int rows_per_wg);
-hipError_t launch_persist(int KC, int K, int prio, int dom, bool lab, bool fast53, const PersistArgs &a, size_t lds,
-                          hipStream_t score_stream, hipStream_t commit_stream, hipStream_t merge_stream);
+// The persistent pipeline (ksched_pipe.hip): ONE kernel of 1 + G workgroups x kPipeThreads, workgroup 0
+// the commit, workgroup 1 + g score waves (0 .. kPipeScoreWaves-1) + merge waves (the rest).
+constexpr int kPipeThreads = 768;
+constexpr int kPipeWaves = kPipeThreads / 64;
+constexpr int kPipeScoreWaves = 8;
+constexpr int kPipeMergeThreads = (kPipeWaves - kPipeScoreWaves) * 64;  // one per score workgroup's list
+struct PipeInfo {
+    size_t lds;         // dynamic LDS per workgroup (max of the commit's and a score workgroup's layout)
+    size_t static_lds;
+    int vgprs;
+    size_t spill;       // private (scratch) bytes per thread
+};
+// launch: 0 = query PipeInfo only, 1 = cooperative launch (the runtime checks the grid against the
+// occupancy query), 2 = plain launch (ranks sharing one device, each with a fraction of the CUs).
+// hipErrorNotSupported: no instantiation for (KC, K) -- the caller runs the stream pipeline.
+hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                           hipStream_t s);
+hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                             hipStream_t s);
+hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                              hipStream_t s);
+inline hipError_t launch_pipe(int KC, int K, int prio, int dom, bool lab, bool f53, const PersistArgs &a, int launch,
+                              PipeInfo *info, hipStream_t s) {
+    if (prio == kPrioPrice) return pipe_part_price(KC, K, lab, false, a, launch, info, s);
+    if (dom == kDomFeasible) return pipe_part_res_feas(KC, K, lab, f53, a, launch, info, s);
+    return pipe_part_res_all(KC, K, lab, f53, a, launch, info, s);
+}
 hipError_t launch_apply_batch(const XBuf *x, NodeRec *nodes, int64_t node_lo, int64_t n_local, hipStream_t s);
 // diagnostics: qdiv(a, b, recip(b)) against the native a / b, bit for bit
 hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, double *native, double *fast,

@@ -364,34 +364,18 @@ __device__ __forceinline__ void score_topk_body(const ScoreArgs &A) {
     }
 }
 
-// Device-side hand-off score(b) -> merge(b) (MI355X_MICROARCH "valid forms", producer side): every
-// storing wave drains its stores, the workgroup meets, lane 0 writes back the XCD L2 (agent release),
-// drains that, then adds to the monotone counter Ctl::scored.  The merge polls the counter instead of
-// waiting on a cross-queue event.
-__device__ __forceinline__ void signal_scored(unsigned long long *done) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-
-
 template <int KC, int K>
 __global__ __launch_bounds__(kMergeThreads) void k_merge_pod(MergeArgs A) {
-    merge_pod_body<KC, K>(A, blockIdx.x);
+    __shared__ MergeSmem<KC, K, kMergeThreads> sm;
+    merge_pod_body<KC, K, false, kMergeThreads>(A, blockIdx.x, threadIdx.x, sm, BlockSync{});
 }
 
-// Score kernel (the merge waits on a stream event, or polls Ctl::scored when A.done is set).
+// Score kernel (the merge waits on a stream event).
 // <= 64 VGPRs (launch bound: 8 waves per SIMD): two score waves + two commit waves (190 VGPRs) must
 // fit one SIMD, or the single-workgroup commit cannot dispatch beside the score grid.
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
 __global__ __launch_bounds__(kScoreThreads, 8) void k_score_topk(ScoreArgs A) {
-    score_topk_body<KC, PRIO, DOM, LAB, F53>(A);  // every path (stale plan included) reaches the signal
-    if (A.done) signal_scored(A.done);
+    score_topk_body<KC, PRIO, DOM, LAB, F53>(A);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -21,24 +21,6 @@ __device__ __forceinline__ void list_insert_ordered(double (&key)[KC], int32_t (
     }
 }
 
-// Consumer side: one relaxed (sc1) poll with s_sleep, one agent acquire, drain, workgroup barrier.  A
-// wall-clock timeout (2 s) sets the device error word instead of spinning forever.
-__device__ __forceinline__ void wait_scored(const unsigned long long *ctr, unsigned long long target, int32_t *err) {
-    if (threadIdx.x == 0) {
-        const uint64_t t0 = wall_clock64();
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(2);
-            if (wall_clock64() - t0 > 200000000ull) {
-                if (err) __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-}
-
 // ------------------------------------------------------------------------------------------------
 // Merge of one pod's workgroup lists (C_in <= 512 lists of KC entries, cut when full) into its K-entry
 // Rec list: one 512-thread workgroup per pod, thread = list.  Selection by RANK, every compare
@@ -55,38 +37,57 @@ __device__ __forceinline__ bool code_better(uint64_t ca, int32_t ia, uint64_t cb
     return ca > cb || (ca == cb && ia < ib);
 }
 
-template <int KC, int K, bool COH = false>
-__device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) {
-    // latency-critical: win issue arbitration over co-resident score waves (low_prio 1/2/3: issue priority
-    // 0/1/2 instead of 3, A/B of how much the merge may take from the score waves sharing its SIMDs)
-    switch (A.low_prio) {
-        case 1: __builtin_amdgcn_s_setprio(0); break;
-        case 2: __builtin_amdgcn_s_setprio(1); break;
-        case 3: __builtin_amdgcn_s_setprio(2); break;
-        default: __builtin_amdgcn_s_setprio(3); break;
-    }
-    constexpr int W = kMergeThreads / 64;
-    __shared__ uint64_t s_code[kMergeThreads][KC];  // every list, as key codes (0 = empty)
-    __shared__ int32_t s_idx[kMergeThreads][KC];
-    __shared__ uint64_t s_ccode[W * K];             // surviving heads
-    __shared__ int32_t s_cidx[W * K], s_clist[W * K];
-    __shared__ int32_t s_keep[K];                   // list of global head rank g
-    __shared__ uint64_t s_ecode[K * KC];            // the kept lists' entries
-    __shared__ int32_t s_eidx[K * KC];
-    __shared__ uint64_t s_ocode[K];
-    __shared__ int32_t s_oidx[K];
-    __shared__ uint64_t s_wck[W];
-    __shared__ int32_t s_wci[W], s_wcut[W], s_wnv[W];
-    __shared__ int64_t s_wcnt[W];
-    const int tid = threadIdx.x;
+// The merge's LDS (one pod at a time): MT lists of KC entries as key codes, plus the rank stages.
+template <int KC, int K, int MT>
+struct MergeSmem {
+    static constexpr int W = MT / 64;
+    uint64_t code[MT][KC];  // every list, as key codes (0 = empty)
+    int32_t idx[MT][KC];
+    uint64_t ccode[W * K];  // surviving heads
+    int32_t cidx[W * K], clist[W * K];
+    int32_t keep[K];        // list of global head rank g
+    uint64_t ecode[K * KC]; // the kept lists' entries
+    int32_t eidx[K * KC];
+    uint64_t ocode[K];
+    int32_t oidx[K];
+    uint64_t wck[W];
+    int32_t wci[W], wcut[W], wnv[W];
+    int64_t wcnt[W];
+};
+
+struct BlockSync {
+    __device__ void operator()() const { __syncthreads(); }
+};
+
+// tid: this thread's index among the MT merging threads; sync(): a barrier of exactly those threads
+// (the whole workgroup in k_merge_pod, the merge waves of a pipeline workgroup in k_pipe).
+template <int KC, int K, bool COH, int MT, typename Sync>
+__device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b, const int tid, MergeSmem<KC, K, MT> &sm,
+                                               Sync sync) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    constexpr int W = MT / 64;
+    auto &s_code = sm.code;
+    auto &s_idx = sm.idx;
+    auto &s_ccode = sm.ccode;
+    auto &s_cidx = sm.cidx;
+    auto &s_clist = sm.clist;
+    auto &s_keep = sm.keep;
+    auto &s_ecode = sm.ecode;
+    auto &s_eidx = sm.eidx;
+    auto &s_ocode = sm.ocode;
+    auto &s_oidx = sm.oidx;
+    auto &s_wck = sm.wck;
+    auto &s_wci = sm.wci;
+    auto &s_wcut = sm.wcut;
+    auto &s_wnv = sm.wnv;
+    auto &s_wcnt = sm.wcnt;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const bool dbg = A.dbg != nullptr;
     uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
     const int64_t p0 = A.p0_known ? A.p0v : load_i64<COH>(A.cursor);
-    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // workgroup-uniform
-    if (A.wait_ctr) wait_scored(A.wait_ctr, A.wait_target, A.err);
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // uniform over the merging threads
     const bool has = tid < A.C_in;
     uint64_t code[KC];
     int32_t idx[KC];
@@ -127,7 +128,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         const int nv = __popcll(__ballot(idx[0] != kNoIdx));
         if (lane == 0) { s_wck[wave] = bc; s_wci[wave] = bi; s_wcut[wave] = wcut; s_wcnt[wave] = wc; s_wnv[wave] = nv; }
     }
-    __syncthreads();
+    sync();
     // 1. rank each head within its wave (broadcast reads, independent compares; waves without lists idle)
     const int nw = (A.C_in + 63) / 64 < W ? (A.C_in + 63) / 64 : W;
     if (wave < nw) {
@@ -143,7 +144,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         }
     }
     if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
+    sync();
     if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
     // 2. rank the survivors against each other
     int ntot = 0;  // valid heads in total (survivors: the first min(K, nv) slots of each wave)
@@ -161,7 +162,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         }
     }
     if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
+    sync();
     // 3. gather the kept lists' entries (empty slots never rank), then rank them against each other
     const int nkeep = ntot < K ? ntot : K;
     const int ne = nkeep * KC;
@@ -171,7 +172,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         s_ecode[tid] = in ? s_code[l][tid % KC] : 0ull;
         s_eidx[tid] = in ? s_idx[l][tid % KC] : kNoIdx;
     }
-    __syncthreads();
+    sync();
     int nvalid = 0;
     if (tid < ne) {
         const uint64_t mc = s_ecode[tid];
@@ -192,7 +193,7 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b) 
         nvalid = cntv;
     }
     if (dbg) ts[5] = __builtin_amdgcn_s_memtime();
-    __syncthreads();
+    sync();
     if (wave != 0) return;
     uint64_t gk = 0ull;
     int32_t gi = kNoIdx;

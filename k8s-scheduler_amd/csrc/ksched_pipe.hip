@@ -1,0 +1,729 @@
+// ksched_pipe.hip -- the batched pipeline as ONE persistent kernel.
+//
+// k_pipe, 1 + G workgroups of 1024 threads, one per CU (its LDS request excludes a second one), every
+// workgroup resident for the whole call -- guaranteed by the launch itself: a cooperative launch of a
+// grid that the occupancy query admits (nothing of the call runs beside it), so no protocol below
+// assumes a dispatch order, a co-location or a second kernel.  Roles come from blockIdx / wave:
+//
+//   workgroup 0          the COMMIT (all 16 waves): per active batch, wait for its B merges, replay the
+//                        batch in pod order against the exact current state (commit_spc_batch), export
+//                        the touched nodes, plan batch b + 2, publish Ctl::committed = b + 1.
+//   workgroup 1 + g      waves 0..7: SCORE -- the rows j = g (mod G) of this rank's nodes live in LDS for
+//                        the whole call; per batch wait for commit(b - 2), apply its export to the rows,
+//                        score 64 pods x the rows (lane = pod), fold the wave lists to one top-KC list per
+//                        pod, store it, arrive.
+//                        waves 8..15 (g < B only): MERGE pod g (g + G, ...) of every batch: wait for the G
+//                        arrivals, merge the G lists into the pod's K-entry Rec list [R > 1: exchange with
+//                        the peer ranks + rank merge], count the merge.
+//
+// The two roles of a score workgroup run independent loops, so they never meet at s_barrier (which
+// would need every wave of the workgroup): each role synchronises its own waves through an LDS counter
+// (role_sync).  Every cross-workgroup hand-off is MI355X_MICROARCH "valid forms" row 1 (sc1 stores,
+// every storing wave drained, one lane's counter update; sc1 loads after the poll) and every wait is
+// bounded (PersistArgs::timeout_ticks -> error words 5..11).  Snapshot semantics: score(b) sees every
+// commit up to b - 2, commit(b) inherits b - 1's (oracle/cpu_ref.c or_schedule_pipelined).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "ksched_commit.h"
+#include "ksched_merge.h"
+
+#ifndef KSCHED_PIPE_PART
+#define KSCHED_PIPE_PART 0
+#endif
+
+namespace ksched {
+
+namespace {
+
+constexpr int kSW = kPipeScoreWaves;  // score waves per workgroup
+constexpr int kMW = kPipeWaves - kSW;  // merge waves
+constexpr int kMT = kMW * 64;          // merging threads: one per score workgroup's list (G <= kMT)
+constexpr int kPU = 4;                 // rows per score step (independent key chains)
+
+// ---- barrier of ONE role's waves (LDS counter; s_barrier would wait for the other role too) ----------
+__device__ __forceinline__ void role_sync(unsigned *ctr, unsigned &target, unsigned nwaves) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    target += nwaves;
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// per-workgroup control words (LDS offset 0 of a score workgroup)
+struct alignas(16) PipeCtl {
+    unsigned sbar, mbar;          // role barrier counters
+    int32_t s_stop, m_stop;
+    int64_t s_p0, s_done;         // score role: this batch's plan and the cursor after commit(b-2)
+    int64_t m_p0, m_done;         // merge role: the same, read by its own poll
+    int32_t c_stop, pad;          // commit workgroup
+};
+constexpr size_t kPipeCtlBytes = 64;
+static_assert(sizeof(PipeCtl) <= kPipeCtlBytes, "PipeCtl");
+
+__device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const unsigned long long *p,
+                                        unsigned long long v, unsigned long long *seen) {
+    return poll_ge(p, v, P.timeout_ticks, &P.ctl->polls_rmw, seen, P.prog ? P.prog + kProgWords * slot + 2 : nullptr);
+}
+
+// the first failure names the wait that timed out (ksched_sync reports it)
+__device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
+
+// Cross-device granules: system-scope relaxed 8-byte accesses (global_store/load ... sc0 sc1) on the
+// uncached receive rings; an 8-byte store arrives whole, so a granule whose tag matches holds its word.
+__device__ __forceinline__ void st_sys(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// poll one granule until it carries `tag` (false: timed out)
+__device__ __forceinline__ bool granule_wait(const uint64_t *p, uint32_t tag, int64_t limit, uint32_t *word) {
+    uint64_t v = ld_sys(p);
+    if ((uint32_t)(v >> 32) != tag) {
+        const uint64_t t0 = wall_clock64();
+        do {
+            if ((int64_t)(wall_clock64() - t0) > limit) return false;
+            __builtin_amdgcn_s_sleep(1);
+            v = ld_sys(p);
+        } while ((uint32_t)(v >> 32) != tag);
+    }
+    *word = (uint32_t)v;
+    return true;
+}
+
+// Rank merge of pod m's R exchanged lists (one wave, lane = source rank; the stream pipeline's
+// k_merge<INPUT_REC> rule): K rounds of wave arg-best over the lists' heads, entries ranking below the
+// best cutoff of a cut list dropped, cut when any input was cut or entries were left over.
+template <int K>
+__device__ __forceinline__ void rank_merge_msgs(const uint32_t *all, int R, Rec *out, int64_t *out_fc) {
+    constexpr int MW = msg_words(K);
+    const int lane = threadIdx.x & 63;
+    const bool has = lane < R;
+    const uint32_t *msg = all + (has ? lane : 0) * MW;
+    auto rec_key = [&](int q) {
+        return __longlong_as_double((long long)(((uint64_t)msg[q * kRecWords + 1] << 32) | msg[q * kRecWords]));
+    };
+    int n = 0;
+    if (has) {
+#pragma unroll
+        for (int q = 0; q < K; ++q) n += msg[q * kRecWords + 3] != 0;  // valid entries form a prefix
+    }
+    const bool cut = has && msg[13] != 0;  // entry 0's pad (Rec word 13)
+    int64_t cnt = has ? (int64_t)(((uint64_t)msg[K * kRecWords + 1] << 32) | msg[K * kRecWords]) : 0;
+    cnt = wave_sum_i64(cnt);
+    double ck = (cut && n > 0) ? rec_key(n - 1) : -__builtin_inf();
+    int32_t ci = (cut && n > 0) ? (int32_t)msg[(n - 1) * kRecWords + 2] : kNoIdx;
+    const bool anycut = __ballot(cut) != 0;
+    {
+        int32_t aux = 0;
+        wave_argbest(ck, ci, aux);
+    }
+    int h = 0;
+    double mk = -__builtin_inf();
+    int32_t mi = kNoIdx, msrc = -1;
+    for (int r = 0; r < K; ++r) {
+        double k = (h < n) ? rec_key(h) : -__builtin_inf();
+        int32_t ix = (h < n) ? (int32_t)msg[h * kRecWords + 2] : kNoIdx;
+        int32_t src = lane * K + h;
+        wave_argbest(k, ix, src);
+        if (ix == kNoIdx) break;  // wave-uniform
+        if (src == lane * K + h) ++h;
+        if (lane == r) { mk = k; mi = ix; msrc = src; }
+    }
+    const bool left = __ballot(h < n) != 0;
+    if (anycut && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
+    const int32_t cut_out = (anycut || left) ? 1 : 0;
+    if (lane < K) {
+        Rec r{};
+        if (mi != kNoIdx) {
+            uint32_t *w = reinterpret_cast<uint32_t *>(&r);
+            const uint32_t *sw = all + (msrc / K) * MW + (msrc % K) * kRecWords;
+#pragma unroll
+            for (int x = 0; x < kRecWords; ++x) w[x] = sw[x];
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        r.pad = lane == 0 ? cut_out : 0;
+        store_rec<true>(out + lane, r);
+    }
+    if (lane == 0) store_i64<true>(out_fc, cnt);
+}
+
+__device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int64_t a2) {
+    nd->a[0] = a0; nd->a[1] = a1; nd->a[2] = a2;
+    const double f0 = (double)a0, f1 = (double)a1, f2 = (double)a2;
+    nd->af[0] = f0; nd->af[1] = f1; nd->af[2] = f2;
+    nd->y[0] = recip_or_zero(a0, f0); nd->y[1] = recip_or_zero(a1, f1); nd->y[2] = recip_or_zero(a2, f2);
+}
+
+// LDS layout of a score workgroup: PipeCtl | rows [R] | fold lists | merge scratch | exchange messages
+template <int KC, int K>
+struct ScoreLayout {
+    static constexpr size_t fold_bytes = (size_t)(kSW / 2) * KC * 64 * 12 + 64 * 4;
+    static constexpr size_t merge_bytes = (sizeof(MergeSmem<KC, K, kMT>) + 15) / 16 * 16;
+    static constexpr size_t msg_bytes = ((size_t)(1 + kMaxXchgRanks) * msg_words(K) * 4 + 15) / 16 * 16;
+    __host__ __device__ static size_t rows_off() { return kPipeCtlBytes; }
+    __host__ __device__ static size_t fold_off(int R) { return kPipeCtlBytes + (size_t)R * sizeof(NodeRec); }
+    __host__ __device__ static size_t merge_off(int R) { return fold_off(R) + (fold_bytes + 15) / 16 * 16; }
+    __host__ __device__ static size_t msg_off(int R) { return merge_off(R) + merge_bytes; }
+    __host__ __device__ static size_t total(int R) { return msg_off(R) + msg_bytes; }
+};
+
+constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16; }
+template <int K>
+constexpr size_t commit_total_bytes() { return commit_loc_bytes() + spc_lds_bytes<K, kPipeThreads>(); }
+
+// ------------------------------------------------------------------------------------------------
+// SCORE role (waves 0 .. kSW-1 of workgroup 1 + g)
+// ------------------------------------------------------------------------------------------------
+template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
+__device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, const int g) {
+    PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
+    const int R = P.rows_per_wg;
+    NodeRec *rows = reinterpret_cast<NodeRec *>(smem + ScoreLayout<KC, K>::rows_off());
+    char *fold = smem + ScoreLayout<KC, K>::fold_off(R);
+    double *s_key = reinterpret_cast<double *>(fold);                     // [W/2][KC][64]
+    int32_t *s_idx = reinterpret_cast<int32_t *>(fold + (size_t)(kSW / 2) * KC * 64 * 8);
+    int32_t *s_cnt = s_idx + (size_t)(kSW / 2) * KC * 64;                 // [64]
+    constexpr int kST = kSW * 64;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int G = P.G;
+    const int64_t n = P.n_local, NP = P.pods.p;
+    Ctl *ctl = P.ctl;
+    unsigned bar = 0;
+    auto sync = [&]() { role_sync(&pc->sbar, bar, kSW); };
+    // this workgroup's rows j = g + r * G, resident in LDS for the whole call
+    for (int e = tid; e < R * 6; e += kST) {
+        const int r = e / 6, piece = e % 6;
+        const int64_t j = g + (int64_t)r * G;
+        if (j < n) reinterpret_cast<int4 *>(rows + r)[piece] = reinterpret_cast<const int4 *>(P.nodes + j)[piece];
+    }
+    sync();
+    const double y3 = recip(3.0);
+    int64_t nact = 0;
+    int idle = 0;
+    for (int64_t b = 0;; ++b) {
+        // ---- wave 0: wait for commit(b-2), then ONE round of loads -- its plan for b, the cursor after it,
+        // its export (count and entries, lane = entry) -- and apply the exported nodes this workgroup owns
+        // to its LDS rows before the barrier (the other waves never touch the export) ----
+        if (wave == 0) {
+            int stop = 0;
+            if (lane == 0) {
+                unsigned long long seen = 0;
+                prog_at(P, g, b, kProgWaitCommit, 0);
+                if (b >= 2 && !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
+                    set_err(P.err, 6);
+                    prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
+                    stop = 2;
+                }
+                if (g == 0) trace_at(P, b, 6);
+            }
+            stop = __builtin_amdgcn_readfirstlane(stop);
+            int64_t p0v = 0, donev = 0;
+            int errv = 0, nxv = 0;
+            uint64_t w0 = 0, w4 = 0, w5 = 0, w6 = 0;
+            const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= 2 ? b - 2 : 0) % 4) * P.xbuf_bytes);
+            if (lane == 0) {
+                p0v = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+                donev = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+                // a failed peer (a wait timed out) ends the call for everyone
+                errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (b >= 2 && !stop) {
+                nxv = (int)(uint32_t)ld_coh(&xb->count);  // one address: one request for the wave
+                if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
+                    const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[lane]);
+                    w0 = ld_coh(w); w4 = ld_coh(w + 4); w5 = ld_coh(w + 5); w6 = ld_coh(w + 6);
+                }
+            }
+            auto apply = [&](uint64_t x0, uint64_t x4, uint64_t x5, uint64_t x6) {
+                const int64_t j = (int64_t)(int32_t)(uint32_t)x0 - P.node_offset;  // local row
+                if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
+                set_row(rows + j / G, (int64_t)x4, (int64_t)x5, (int64_t)x6);
+                // the mergers read a candidate's state from its HBM row (sc1)
+                st_coh(&P.nodes[j].a[0], x4);
+                st_coh(&P.nodes[j].a[1], x5);
+                st_coh(&P.nodes[j].a[2], x6);
+            };
+            if (lane < nxv) apply(w0, w4, w5, w6);
+            for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
+                const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
+                apply(ld_coh(w), ld_coh(w + 4), ld_coh(w + 5), ld_coh(w + 6));
+            }
+            if (lane == 0) {
+                pc->s_p0 = p0v;
+                pc->s_done = donev;
+                pc->s_stop = errv != 0 ? 3 : stop;
+            }
+        }
+        sync();
+        if (pc->s_stop) return;
+        const int64_t p0 = pc->s_p0;
+        if (pc->s_done >= NP) break;  // every pod resolved by commit(b-2) or earlier
+        if (p0 < 0 || p0 >= NP) {     // nothing planned for batch b (identical on every workgroup)
+            if (tid == 0) prog_at(P, g, b, kProgIdle, (uint64_t)p0);
+            // a truncation re-plans within two batches; a longer run of empty plans is a protocol error
+            if (++idle > kPlanRing) {
+                if (tid == 0) set_err(P.err, 8);
+                return;
+            }
+            sync();  // every wave has read s_done before wave 0 rewrites it
+            continue;
+        }
+        idle = 0;
+        ++nact;
+        if (tid == 0) {
+            if (g == 0) trace_at(P, b, 0);
+            prog_at(P, g, b, kProgScan, 0);
+        }
+        const uint64_t t_go = (P.trace && tid == 0) ? wall_clock64() : 0;
+        // ---- score: lane = pod, wave w scans rows r = w, w + W, ... (nodes j = g + r G) ----
+        if (tid < 64) s_cnt[tid] = 0;
+        const int64_t pod = p0 + lane;
+        const bool active = (lane < P.B) && (pod < NP);
+        const int64_t rc = active ? P.pods.rc[pod] : 0;
+        const int64_t rm = active ? P.pods.rm[pod] : 0;
+        const int64_t rp = active ? P.pods.rp[pod] : 0;
+        const uint64_t sel = (LAB && active) ? P.pods.sel[pod] : 0;
+        const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+        double key[KC];
+        int32_t idx[KC];
+#pragma unroll
+        for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
+        int32_t cnt = 0;
+        // kPU rows per step: their keys are independent f64 chains the scheduler interleaves; inserted
+        // in ascending node order afterwards
+        for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
+            double ks[kPU];
+#pragma unroll
+            for (int u = 0; u < kPU; ++u) {
+                const int r = r0 + u * kSW;
+                const int64_t j = g + (int64_t)r * G;
+                ks[u] = -__builtin_inf();
+                if (r < R && j < n) {  // wave-uniform
+                    const NodeRec &nd = rows[r];
+                    const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+                    const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
+                    cnt += f;
+                    double k;
+                    const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0],
+                                                                  nd.af[1], nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3,
+                                                                  nd.price, &k);
+                    ks[u] = el ? k : -__builtin_inf();
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kPU; ++u) {
+                double ck = ks[u];
+                int32_t ci = (int32_t)(P.node_offset + g + (int64_t)(r0 + u * kSW) * G);  // global index
+                bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    const bool sw = moved || ck > key[q];
+                    moved = sw;
+                    const double tk = key[q];
+                    const int32_t ti = idx[q];
+                    key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+                    ck = sw ? tk : ck; ci = sw ? ti : ci;
+                }
+            }
+        }
+        if (g == 0 && tid == 0) trace_at(P, b, 8);
+        const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
+        sync();  // s_cnt zeroed before any wave adds
+        if (g == 0 && tid == 0) trace_at(P, b, 9);
+        if (cnt) atomicAdd(&s_cnt[lane], cnt);
+        // fold the wave lists pairwise: W -> W/2 -> ... -> 1 (a list that is cut when full folds into
+        // the top-KC of the union, again cut when full: DESIGN.md section 4)
+#pragma unroll
+        for (int half = kSW / 2; half >= 1; half >>= 1) {
+            if (wave >= half && wave < 2 * half) {
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    s_key[((wave - half) * KC + q) * 64 + lane] = key[q];
+                    s_idx[((wave - half) * KC + q) * 64 + lane] = idx[q];
+                }
+            }
+            sync();
+            if (wave < half) {
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    const int32_t oi = s_idx[(wave * KC + q) * 64 + lane];
+                    if (oi == kNoIdx) break;
+                    list_insert_ordered<KC>(key, idx, s_key[(wave * KC + q) * 64 + lane], oi);
+                }
+            }
+            if (half > 1) sync();
+        }
+        if (g == 0 && tid == 0) trace_at(P, b, 10);
+        const size_t part_elems = (size_t)P.B * G;
+        Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
+        int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        if (wave == 0) {
+            // s_cnt: every wave added before the last fold barrier
+            if (active) {
+                Cand *dst = part + ((size_t)lane * G + g) * KC;
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    st_coh(&dst[q].key, (uint64_t)__double_as_longlong(key[q]));
+                    st_coh(&dst[q].idx, (uint64_t)(uint32_t)idx[q]);  // idx + pad (0)
+                }
+                st_coh(part_cnt + (size_t)lane * G + g, (uint64_t)(int64_t)s_cnt[lane]);
+            }
+            drain_stores();
+            // ---- arrive (the merge waves of workgroups 1 .. B wait for all G); wave 0 made every store ----
+            const int slot = (int)((nact - 1) % 4);
+            if (lane == 0) {
+                if (g == 0) trace_at(P, b, 5);
+                const unsigned long long old = __hip_atomic_fetch_add(&ctl->arrive[slot].v, 1ull, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long use = (unsigned long long)((nact - 1) / 4);
+                if (old + 1 == (use + 1) * (unsigned long long)G) trace_at(P, b, 1);
+                prog_at(P, g, b, kProgArrived, old + 1);
+                if (P.trace) prog_add(P, g, t_scan - t_go, wall_clock64() - t_go);
+            }
+        }
+        // the next batch's first barrier orders s_cnt / fold reuse after wave 0's reads
+    }
+    // every pod is resolved: this workgroup's rows go back to HBM whole (allocatable, cached doubles,
+    // reciprocals) for the next call and for ksched_read_nodes
+    for (int e = tid; e < R * 6; e += kST) {
+        const int r = e / 6, piece = e % 6;
+        const int64_t j = g + (int64_t)r * G;
+        if (j < n) reinterpret_cast<int4 *>(P.nodes + j)[piece] = reinterpret_cast<const int4 *>(rows + r)[piece];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// MERGE role (waves kSW .. 15 of workgroup 1 + g, g < B): pods m = g, g + G, ... of every batch
+// ------------------------------------------------------------------------------------------------
+template <int KC, int K>
+__device__ __forceinline__ void merge_role(const PersistArgs &P, char *smem, const int g) {
+    PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
+    const int R = P.rows_per_wg;
+    MergeSmem<KC, K, kMT> &ms = *reinterpret_cast<MergeSmem<KC, K, kMT> *>(smem + ScoreLayout<KC, K>::merge_off(R));
+    uint32_t *s_msg = reinterpret_cast<uint32_t *>(smem + ScoreLayout<KC, K>::msg_off(R));  // this rank's list
+    uint32_t *s_all = s_msg + msg_words(K);                                                  // every rank's list
+    const int mtid = threadIdx.x - kSW * 64;
+    const int G = P.G;
+    const int slot_prog = G + g;
+    const int64_t NP = P.pods.p;
+    Ctl *ctl = P.ctl;
+    unsigned bar = 0;
+    auto sync = [&]() { role_sync(&pc->mbar, bar, kMW); };
+    int64_t nact = 0;
+    int idle = 0;
+    for (int64_t b = 0;; ++b) {
+        if (mtid == 0) {
+            int stop = 0;
+            unsigned long long seen = 0;
+            prog_at(P, slot_prog, b, kProgWaitCommit, 0);
+            if (b >= 2 && !spin_ge(P, slot_prog, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1),
+                                   &seen)) {
+                set_err(P.err, 6);
+                prog_at(P, slot_prog, b, kProgWaitCommit | kProgTimedOut, seen);
+                stop = 2;
+            }
+            pc->m_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+            pc->m_done = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+            if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
+            pc->m_stop = stop;
+        }
+        sync();
+        if (pc->m_stop) return;
+        const int64_t p0 = pc->m_p0;
+        if (pc->m_done >= NP) return;
+        if (p0 < 0 || p0 >= NP) {
+            if (mtid == 0) prog_at(P, slot_prog, b, kProgIdle, (uint64_t)p0);
+            if (++idle > kPlanRing) {
+                if (mtid == 0) set_err(P.err, 8);
+                return;
+            }
+            sync();  // m_p0 / m_done are rewritten next iteration
+            continue;
+        }
+        idle = 0;
+        ++nact;
+        const int slot = (int)((nact - 1) % 4);
+        const unsigned long long use = (unsigned long long)((nact - 1) / 4);
+        if (mtid == 0) {
+            unsigned long long seen = 0;
+            prog_at(P, slot_prog, b, kProgWaitArrive, 0);
+            pc->m_stop = spin_ge(P, slot_prog, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, &seen) ? 0 : 1;
+            if (pc->m_stop) {
+                set_err(P.err, 7);
+                prog_at(P, slot_prog, b, kProgWaitArrive | kProgTimedOut, seen);
+            }
+            if (g == 0) trace_at(P, b, 7);
+        }
+        sync();
+        if (pc->m_stop) return;
+        const size_t part_elems = (size_t)P.B * G;
+        char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
+        MergeArgs ma{};
+        ma.in = P.part + (size_t)(b % 2) * part_elems * KC;
+        ma.in_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
+        ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
+        ma.p0_known = 1; ma.p0v = p0;
+        ma.nodes = P.nodes; ma.node_offset = P.node_offset;
+        ma.dbg = P.mdbg;
+        ma.out_rec = reinterpret_cast<Rec *>(lb);
+        ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
+        for (int m = g; m < P.B; m += G) {
+            const bool xchg = P.R > 1 && p0 + m < NP;  // uniform over the merge waves
+            ma.lds_msg = xchg ? s_msg : nullptr;
+            merge_pod_body<KC, K, true, kMT>(ma, m, mtid, ms, sync);
+            if (xchg) {
+                // this rank's list of pod m -> slot (a % 4, rank, m) of every rank's ring; then the R lists of
+                // pod m from this rank's ring -> rank merge -> the commit's list (lring)
+                constexpr int MW = msg_words(K);
+                const int RR = P.R;
+                const uint32_t tag = P.epoch0 + (uint32_t)nact;
+                sync();
+                for (int e = mtid; e < MW * RR; e += kMT) {
+                    const int r = e / MW, w = e % MW;
+                    uint64_t *dst = reinterpret_cast<uint64_t *>(
+                        P.rx_peer[r] + ((size_t)(slot * RR + P.rank) * P.B + m) * (size_t)P.xchg_stride);
+                    st_sys(dst + w, (uint64_t)s_msg[w] | ((uint64_t)tag << 32));
+                }
+                bool ok = true;
+                const char *own = P.rx_peer[P.rank];
+                for (int e = mtid; e < MW * RR; e += kMT) {
+                    const int r = e / MW, w = e % MW;
+                    const uint64_t *src = reinterpret_cast<const uint64_t *>(
+                        own + ((size_t)(slot * RR + r) * P.B + m) * (size_t)P.xchg_stride);
+                    uint32_t word = 0;
+                    if (ok && !granule_wait(src + w, tag, P.timeout_ticks, &word)) ok = false;
+                    s_all[e] = word;
+                }
+                if (!ok) { set_err(P.err, 10); pc->m_stop = 1; }
+                sync();
+                if (pc->m_stop) return;
+                if (mtid < 64) rank_merge_msgs<K>(s_all, RR, ma.out_rec + (size_t)m * K, ma.out_fc + m);
+            }
+            drain_stores();
+            sync();  // every merge wave's stores drained before the count; LDS free for the next pod
+            if (mtid == 0) {
+                if (m == 0) st_coh(&ctl->nact, (uint64_t)nact);
+                const unsigned long long d =
+                    __hip_atomic_fetch_add(&ctl->merged[slot].v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (d + 1 == (use + 1) * (unsigned long long)P.B) trace_at(P, b, 2);
+                prog_at(P, slot_prog, b, kProgMerged, d + 1);
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// COMMIT role (workgroup 0, all 16 waves): batch after batch, wait for the B merges of an active batch
+// (Ctl::merged), commit it (commit_spc_batch: lists read with sc1 loads; export, plans and cursor left as
+// sc1 stores), publish Ctl::committed.  Once every pod is resolved it publishes a committed count no wait
+// can exceed, so every workgroup still waiting sees the end.
+// ------------------------------------------------------------------------------------------------
+template <int K, int PRIO, int DOM, bool LAB, bool F53>
+__device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
+    __builtin_amdgcn_s_setprio(3);
+    PersistLocal &loc = *reinterpret_cast<PersistLocal *>(smem);
+    char *cs = smem + commit_loc_bytes();
+    __shared__ int s_stop;
+    Ctl *ctl = P.ctl;
+    // k_ctl_init ran before this kernel on the stream: take the initial plans / cursor / stats once
+    if (threadIdx.x < kPlanRing) loc.plan[threadIdx.x] = (int64_t)ld_rmw(&ctl->plan[threadIdx.x]);
+    if (threadIdx.x == 0) {
+        loc.cursor = (int64_t)ld_rmw(&ctl->cursor);
+        for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_rmw(&ctl->stats[i]);
+        loc.xcount = 0;
+    }
+    __syncthreads();
+    const int cslot = P.G + P.B;  // progress slot
+    int64_t nact = 0;
+    int idle = 0;
+    for (int64_t b = 0;; ++b) {
+        const int64_t p0 = loc.plan[b % kPlanRing];  // written by this workgroup (or k_ctl_init)
+        if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
+            // pods remain but nothing is planned: a truncation re-plans within two batches, so this is a
+            // protocol error -- stop everyone instead of spinning
+            if (threadIdx.x == 0) atomicCAS(P.err, 0, 9);
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
+            return;
+        }
+        LanePods pre{0, 0, 0, 0};
+        const bool act = p0 >= 0 && p0 < P.pods.p;
+        if (act) {
+            idle = 0;
+            ++nact;
+            // the pods' requests are known now: their loads overlap the inherited-slot work
+            if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
+        }
+        // the batch's merges (everything of the commit that needs no candidate list runs before this)
+        auto wait_merged = [&]() -> bool {
+            if (act) {
+                if (threadIdx.x == 0) {
+                    const int slot = (int)((nact - 1) % 4);
+                    const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
+                    unsigned long long seen = 0;
+                    prog_at(P, cslot, b, kProgWaitMerged, 0);
+                    s_stop = poll_ge(&ctl->merged[slot].v, want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
+                    if (s_stop) prog_at(P, cslot, b, kProgWaitMerged | kProgTimedOut, seen);
+                }
+                __syncthreads();
+                if (s_stop) return false;
+            }
+            if (threadIdx.x == 0) trace_at(P, b, 3);
+            return true;
+        };
+        CommitArgs ca{};
+        char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
+        ca.lists = reinterpret_cast<const Rec *>(lb);
+        ca.fc0 = reinterpret_cast<const int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
+        ca.pods = P.pods; ca.ctl = ctl; ca.B = P.B;
+        ca.plan = &ctl->plan[b % kPlanRing];
+        ca.plan1 = &ctl->plan[(b + 1) % kPlanRing];
+        ca.plan2 = &ctl->plan[(b + 2) % kPlanRing];
+        ca.xin = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes);
+        ca.xout = reinterpret_cast<XBuf *>(P.xring + (size_t)(b % 4) * P.xbuf_bytes);
+        ca.out = P.out;
+        ca.batch = b;
+        ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
+        ca.dbg = P.cdbg;
+        ca.loc = &loc;
+        if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged)) {
+            if (threadIdx.x == 0) atomicCAS(P.err, 0, 5);
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
+            return;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            trace_at(P, b, 4);
+            prog_at(P, cslot, b, kProgCommitted, 0);
+        }
+        if (loc.cursor >= P.pods.p) {
+            if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
+            return;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The kernel.  <= 128 VGPRs (1024 threads: four waves per SIMD).
+// ------------------------------------------------------------------------------------------------
+template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(kPipeThreads) void k_pipe(PersistArgs P) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if (blockIdx.x == 0) {
+#ifndef KSCHED_PROBE_NO_COMMIT
+        commit_role<K, PRIO, DOM, LAB, F53>(P, smem);
+#endif
+        return;
+    }
+    const int g = blockIdx.x - 1;
+    PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
+    if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
+    __syncthreads();  // the only workgroup-wide barrier: before the roles part
+#ifndef KSCHED_PROBE_NO_SCORE
+    if (threadIdx.x < kSW * 64) score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, g);
+#endif
+#ifndef KSCHED_PROBE_NO_MERGE
+    if (threadIdx.x >= kSW * 64 && g < P.B) merge_role<KC, K>(P, smem, g);
+#endif
+}
+
+template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t pipe_one(const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+    auto fn = k_pipe<KC, K, PRIO, DOM, LAB, F53>;
+    const size_t sl = ScoreLayout<KC, K>::total(a.rows_per_wg), cl = commit_total_bytes<K>();
+    const size_t lds = sl > cl ? sl : cl;
+    if (info) {
+        hipFuncAttributes at{};
+        hipError_t e = hipFuncGetAttributes(&at, (const void *)fn);
+        if (e != hipSuccess) return e;
+        info->lds = lds;
+        info->static_lds = at.sharedSizeBytes;
+        info->vgprs = at.numRegs;
+        info->spill = at.localSizeBytes;
+    }
+    if (!launch) return hipSuccess;
+    if (a.G > kMT || a.B > 64) return hipErrorInvalidValue;
+    hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    if (launch == 1) {
+        void *args[] = {const_cast<PersistArgs *>(&a)};
+        return hipLaunchCooperativeKernel((const void *)fn, dim3(1 + a.G), dim3(kPipeThreads), args, (unsigned)lds, s);
+    }
+    hipLaunchKernelGGL(fn, dim3(1 + a.G), dim3(kPipeThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t pipe_kk(int KC, int K, const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+    if (KC == 4 && K == 4) return pipe_one<4, 4, PRIO, DOM, LAB, F53>(a, launch, info, s);
+    if (KC == 4 && K == 8) return pipe_one<4, 8, PRIO, DOM, LAB, F53>(a, launch, info, s);
+    if (KC == 4 && K == 16) return pipe_one<4, 16, PRIO, DOM, LAB, F53>(a, launch, info, s);
+    if (KC == 8 && K == 8) return pipe_one<8, 8, PRIO, DOM, LAB, F53>(a, launch, info, s);
+    if (KC == 8 && K == 16) return pipe_one<8, 16, PRIO, DOM, LAB, F53>(a, launch, info, s);
+    return hipErrorNotSupported;
+}
+
+template <int PRIO, int DOM>
+hipError_t pipe_lf(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+    if (PRIO == kPrioPrice) f53 = false;  // best-price never divides
+    if (lab) return f53 ? pipe_kk<PRIO, DOM, true, true>(KC, K, a, launch, info, s)
+                        : pipe_kk<PRIO, DOM, true, false>(KC, K, a, launch, info, s);
+    return f53 ? pipe_kk<PRIO, DOM, false, true>(KC, K, a, launch, info, s)
+               : pipe_kk<PRIO, DOM, false, false>(KC, K, a, launch, info, s);
+}
+
+}  // namespace
+
+#if KSCHED_PIPE_PART == 0
+hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                           hipStream_t s) {
+    return pipe_lf<kPrioPrice, kDomFeasible>(KC, K, lab, f53, a, launch, info, s);
+}
+
+// All ranks meet on the device and agree on the minimum of `mine` (tag: this call's epoch0; the
+// batches of the call use epoch0 + 1, ...).  One wave; lane r < R writes rank r's barrier granule.
+__global__ __launch_bounds__(64) void k_xchg_min(PersistArgs P, int32_t mine, int32_t *out) {
+    const int lane = threadIdx.x;
+    const size_t off = (size_t)4 * P.R * P.B * (size_t)P.xchg_stride;
+    const uint32_t tag = P.epoch0;
+    if (lane < P.R) st_sys(reinterpret_cast<uint64_t *>(P.rx_peer[lane] + off) + P.rank, (uint64_t)(uint32_t)mine | ((uint64_t)tag << 32));
+    int32_t v = 0x7fffffff;
+    bool ok = true;
+    if (lane < P.R) {
+        uint32_t w = 0;
+        ok = granule_wait(reinterpret_cast<const uint64_t *>(P.rx_peer[P.rank] + off) + lane, tag, P.timeout_ticks, &w);
+        v = (int32_t)w;
+    }
+    v = wave_min_i32(v);
+    const bool bad = __ballot(!ok) != 0;
+    if (lane == 0) {
+        if (bad) set_err(P.err, 11);
+        *out = bad ? -1 : v;
+    }
+}
+
+hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hipStream_t s) {
+    if (a.R < 2 || a.R > kMaxXchgRanks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_xchg_min, dim3(1), dim3(64), 0, s, a, mine, out);
+    return hipGetLastError();
+}
+#elif KSCHED_PIPE_PART == 1
+hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                             hipStream_t s) {
+    return pipe_lf<kPrioResource, kDomAll>(KC, K, lab, f53, a, launch, info, s);
+}
+#else
+hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+                              hipStream_t s) {
+    return pipe_lf<kPrioResource, kDomFeasible>(KC, K, lab, f53, a, launch, info, s);
+}
+#endif
+
+}  // namespace ksched

@@ -23,7 +23,9 @@ E_UNKNOWN_NODE = -6
 NO_FIT = -1
 NO_POSITIVE_SCORE = -2
 
+ABI_VERSION = 4
 MODE_EXACT, MODE_BATCHED, MODE_AUTO = 0, 1, 2
+PIPELINE_AUTO, PIPELINE_STREAM = 0, 1
 PRIORITY_RESOURCE, PRIORITY_BEST_PRICE = 0, 1
 DOMAIN_ALL, DOMAIN_FEASIBLE = 0, 1
 REASON_FIT, REASON_CPU, REASON_MEMORY, REASON_POD, REASON_LABELS = 0, 1, 2, 3, 4
@@ -43,7 +45,8 @@ class Opts(C.Structure):
                 ("device", C.c_int32), ("rank", C.c_int32), ("nranks", C.c_int32),
                 ("node_offset", C.c_int64), ("nodes_global", C.c_int64), ("exact_wgs", C.c_int32),
                 ("timing", C.c_int32), ("timing_every", C.c_int32), ("chunk_topk", C.c_int32),
-                ("commit_impl", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("commit_impl", C.c_int32), ("pipeline", C.c_int32), ("pipe_wgs", C.c_int32),
+                ("reserved", C.c_int32 * 1)]
 
 
 class Stats(C.Structure):
@@ -84,6 +87,7 @@ SIGNATURES = [
     ("ksched_xchg_export", C.c_int, [CTX, C.c_char_p]),
     ("ksched_xchg_import", C.c_int, [CTX, C.c_char_p]),
     ("ksched_xchg_ready", C.c_int, [CTX]),
+    ("ksched_xchg_close", C.c_int, [CTX]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
     ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),
@@ -99,6 +103,7 @@ SIGNATURES = [
     ("ksched_download_results", C.c_int, [CTX, C.c_int64, I32P, F64P, I32P]),
     ("ksched_get_stats", C.c_int, [CTX, C.POINTER(Stats)]),
     ("ksched_set_timing", C.c_int, [CTX, C.c_int32, C.c_int32]),
+    ("ksched_set_timeout", C.c_int, [CTX, C.c_int32]),
     ("ksched_selftest_fastdiv", C.c_int, [CTX, C.c_int64, F64P, F64P, F64P, F64P]),
     ("ksched_parse_cpu", C.c_int, [C.c_char_p, I64P]),
     ("ksched_parse_memory", C.c_int, [C.c_char_p, I64P]),
@@ -121,7 +126,7 @@ def lib():
             fn = getattr(lb, name)
             fn.restype = res
             fn.argtypes = args
-        if lb.ksched_abi_version() != 3:
+        if lb.ksched_abi_version() != ABI_VERSION:
             raise ImportError("libksched ABI version mismatch")
         _lib = lb
     return _lib

@@ -43,7 +43,8 @@ def broadcast_bytes(payload, rank: int, src: int = 0) -> bytes:
 def setup_exchange(eng, rank: int, world: int, pg=None) -> bool:
     """Device-side candidate exchange (ksched_xchg_*): every rank exports its receive ring's IPC handle,
     the handles are all-gathered over torch.distributed (`pg`, default group), every rank maps them.
-    All ranks agree on the outcome: if any rank fails, none uses the exchange (False)."""
+    All ranks agree on the outcome: if any rank fails, every rank turns the exchange off again
+    (ksched_xchg_close) and False is returned -- no two ranks ever run different transports."""
     import torch.distributed as dist
     ok, h = 1, b""
     try:
@@ -60,7 +61,10 @@ def setup_exchange(eng, rank: int, world: int, pg=None) -> bool:
             ok = 0
     flags = [None] * world
     dist.all_gather_object(flags, ok, group=pg)
-    return all(flags)
+    agreed = all(flags)
+    if not agreed:
+        eng.xchg_close()
+    return agreed
 
 
 def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group=None, comm: bool = True,
@@ -87,8 +91,9 @@ def make_sharded_engine(cl, rank: int, world: int, device: int, mode=None, group
             uid = Engine.unique_id() if rank == 0 else None
             uid = broadcast_bytes(uid, rank)
             eng.set_comm(uid)
-        if xchg:
-            setup_exchange(eng, rank, world, pg=pg)
+        if xchg and not setup_exchange(eng, rank, world, pg=pg) and not comm:
+            raise RuntimeError("node-sharded engine: the device exchange could not be set up on every rank "
+                               "and no RCCL communicator was requested (comm=False)")
     return eng, (lo, hi)
 
 

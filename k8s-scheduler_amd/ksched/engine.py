@@ -53,7 +53,7 @@ class Engine:
                  use_labels: bool = False, batch: int = 0, topk: int = 0, device: int = -1,
                  rank: int = 0, nranks: int = 1, node_offset: int = 0, nodes_global: int = 0, exact_wgs: int = 0,
                  timing: bool = False, timing_every: int = 0, chunk_topk: int = 0,
-                 commit_impl: int = 0):
+                 commit_impl: int = 0, pipeline: int = L.PIPELINE_AUTO, pipe_wgs: int = 0):
         lb = L.lib()
         o = L.Opts()
         L.check(lb.ksched_default_opts(C.byref(o)), what="default_opts")
@@ -62,6 +62,7 @@ class Engine:
         o.rank, o.nranks, o.node_offset, o.nodes_global, o.exact_wgs = rank, nranks, node_offset, nodes_global, exact_wgs
         o.timing, o.timing_every, o.chunk_topk = int(bool(timing)), timing_every, chunk_topk
         o.commit_impl = commit_impl
+        o.pipeline, o.pipe_wgs = pipeline, pipe_wgs
         ctx = L.CTX()
         L.check(lb.ksched_create(C.byref(o), C.byref(ctx)), what="create")
         self._ctx = ctx
@@ -111,6 +112,10 @@ class Engine:
         blob = b"".join(handles)
         assert len(blob) == L.XCHG_HANDLE_BYTES * self.opts.nranks
         self._chk(L.lib().ksched_xchg_import(self._ctx, blob), "xchg_import")
+
+    def xchg_close(self):
+        """Turn the device exchange off on this rank (the ranks must agree on the transport)."""
+        self._chk(L.lib().ksched_xchg_close(self._ctx), "xchg_close")
 
     @property
     def xchg_ready(self) -> bool:
@@ -210,6 +215,10 @@ class Engine:
     def set_timing(self, on: bool, every: int = 0):
         """Sampled per-kernel HIP-event timing for the following calls (every: one batch in N)."""
         self._chk(L.lib().ksched_set_timing(self._ctx, int(bool(on)), int(every)), "set_timing")
+
+    def set_timeout(self, ms: int):
+        """Bound (ms) of every device-side wait of the persistent pipeline (ksched_set_timeout)."""
+        self._chk(L.lib().ksched_set_timeout(self._ctx, int(ms)), "set_timeout")
 
     def schedule(self, req_cpu, req_mem, req_pods, selector=None):
         """schedulePods over the given pending pods (in order).  Returns (idx, score, feasible)."""

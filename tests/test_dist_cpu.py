@@ -139,11 +139,15 @@ def test_sharded_equals_sequential(oracle_mod, case):
 
 class _FakeXchgEngine:
     """Stands in for ksched.Engine in the exchange setup (CPU): export returns a per-rank handle or
-    fails, import records what it was given."""
+    fails, import records what it was given, close turns the (imported) exchange off again."""
 
     def __init__(self, rank, fail_export=False, fail_import=False):
         self.rank, self.fail_export, self.fail_import = rank, fail_export, fail_import
         self.imported = None
+        self.ready = False
+
+    def xchg_close(self):
+        self.ready = False
 
     def xchg_export(self):
         if self.fail_export:
@@ -154,6 +158,7 @@ class _FakeXchgEngine:
         if self.fail_import:
             raise RuntimeError("cannot map")
         self.imported = list(handles)
+        self.ready = True
 
 
 def _xchg_worker(rank, world, port, fail_rank, fail_where, q):
@@ -168,7 +173,7 @@ def _xchg_worker(rank, world, port, fail_rank, fail_where, q):
         eng = _FakeXchgEngine(rank, fail_export=(rank == fail_rank and fail_where == "export"),
                               fail_import=(rank == fail_rank and fail_where == "import"))
         ok = setup_exchange(eng, rank, world)
-        q.put((rank, ok, eng.imported))
+        q.put((rank, ok, eng.imported, eng.ready))
     finally:
         dist.destroy_process_group()
 
@@ -184,11 +189,13 @@ def test_exchange_setup_agreement(world, fail_rank, fail_where):
     procs = [ctx.Process(target=_xchg_worker, args=(r, world, port, fail_rank, fail_where, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (ok, imp)) for r, ok, imp in (q.get(timeout=120) for _ in range(world)))
+    res = dict((r, (ok, imp, ready)) for r, ok, imp, ready in (q.get(timeout=120) for _ in range(world)))
     for p in procs:
         p.join(timeout=30)
-    oks = {ok for ok, _ in res.values()}
+    oks = {ok for ok, _, _ in res.values()}
     assert oks == {fail_rank < 0}, res
+    # a rank whose import succeeded while a peer failed has closed its exchange again (ksched_xchg_close)
+    assert {ready for _, _, ready in res.values()} == {fail_rank < 0}, res
     if fail_rank < 0:
         for r in range(world):
             assert res[r][1] == [bytes([k]) * 64 for k in range(world)]

@@ -267,38 +267,34 @@ def test_sharded_engine_helper_world1(gpu_available, oracle_mod):
     assert_same((oi, os_, of, st), oracle_mod.schedule(cl), "sharded-helper")
 
 
-@pytest.mark.parametrize("env", [{"KSCHED_PERSIST": "0"}, {"KSCHED_PERSIST": "0", "KSCHED_DEVICE_HANDOFF": "1"},
-                                 {"KSCHED_PERSIST": "0", "KSCHED_SCORE_EVENT": "1"}],
-                         ids=["stream", "stream_merge_poll", "stream_score_event"])
-def test_pipeline_variants_parity(gpu_available, oracle_mod, env, monkeypatch):
-    """Single-rank batched mode runs the persistent pipeline by default (ksched_persist.hip); the stream
-    pipeline (per-batch launches; the multi-rank path) and its alternative hand-offs -- the merge polling
-    Ctl::scored instead of a stream event, the score waiting on a stream event instead of polling
-    Ctl::committed -- stay bit-exact.  Selected by environment switches at enqueue time."""
+def test_stream_pipeline_parity(gpu_available, oracle_mod):
+    """The stream pipeline (per-batch score / merge / commit launches: the RCCL and rank-group multi-rank
+    path, and the single-rank fallback where the persistent kernel does not fit) stays bit-exact;
+    opts.pipeline = KSCHED_PIPELINE_STREAM selects it."""
     from ksched import MODE_BATCHED, cluster
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    from ksched._lib import PIPELINE_STREAM
     for name, nn, pp in (("c3", 30000, 2000), ("c5", 40000, 1500), ("c5hc", 20000, 3000)):
         cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
         want = oracle_mod.schedule(cl, nthreads=8)
-        for kw in (dict(topk=16, batch=64), dict(topk=8, batch=32, chunk_topk=2)):
-            got = run_engine(cl, MODE_BATCHED, **kw)
-            assert_same(got, want, f"{name}/{env}/{kw}")
-            assert got[4]["pipeline"] == "stream", got[4]
+        for kw in (dict(topk=16, batch=64), dict(topk=8, batch=32, chunk_topk=2), dict(topk=16, batch=128)):
+            got = run_engine(cl, MODE_BATCHED, pipeline=PIPELINE_STREAM, **kw)
+            assert_same(got, want, f"{name}/stream/{kw}")
+            assert got[4]["pipeline"] in ("stream", "stream-sequential"), got[4]
 
 
 @pytest.mark.parametrize("name,nn,pp", [("c3", 30000, 2000), ("c5", 40000, 1500), ("c5hc", 20000, 3000),
                                          ("c2", 5000, 2000), ("c1", 700, 300)])
 def test_persistent_pipeline_parity(gpu_available, oracle_mod, name, nn, pp):
-    """The default single-rank batched path is the persistent pipeline (ksched_persist.hip: a resident
-    score grid of up to CUs - 8 workgroups + one resident commit workgroup); the stats say it ran, and it
-    is bit-exact at every (topk, batch, chunk_topk) it accepts -- including the grid sizes where the
-    score workgroups outnumber the batch (non-merger workgroups run a batch ahead)."""
+    """The default batched path is the persistent pipeline (ksched_pipe.hip: ONE cooperative kernel, the
+    commit workgroup + up to CUs - 1 score workgroups whose merge waves merge one pod each); the stats say
+    it ran, and it is bit-exact at every (topk, batch, chunk_topk) it accepts -- including the grid sizes
+    where the score workgroups outnumber the batch (workgroups without a pod to merge run ahead) and
+    small grids where one workgroup merges several pods of a batch (pipe_wgs)."""
     from ksched import MODE_BATCHED, cluster
     cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
     want = oracle_mod.schedule(cl, nthreads=8)
-    for kw in (dict(topk=16, batch=64), dict(topk=8, batch=64, chunk_topk=8), dict(topk=4, batch=32, chunk_topk=2),
-               dict(topk=16, batch=16)):
+    for kw in (dict(topk=16, batch=64), dict(topk=8, batch=64, chunk_topk=8), dict(topk=4, batch=32, chunk_topk=4),
+               dict(topk=16, batch=16), dict(topk=16, batch=64, pipe_wgs=34)):
         got = run_engine(cl, MODE_BATCHED, **kw)
         assert_same(got, want, f"{name}/{kw}")
         assert got[4]["pipeline"] == "persistent", got[4]

@@ -1,8 +1,8 @@
-"""The persistent pipeline's failure path: every wait is bounded, a timeout ends all
-three resident kernels and names where the workgroups stood, and the context stays usable -- the next call
-(persistent, or the stream pipeline the bench falls back to) is bit-exact against the oracle again.
+"""The persistent pipeline's failure path: every wait is bounded, a timeout ends
+every role of the kernel and names where the workgroups stood, and the context stays usable -- the next call
+(persistent, or the stream pipeline) is bit-exact against the oracle again.
 
-The timeout is forced with KSCHED_PERSIST_TIMEOUT_MS=0: every wait not satisfied by its first poll gives up.
+The timeout is forced with ksched_set_timeout(ctx, 0): every wait not satisfied by its first poll gives up.
 """
 import numpy as np
 import pytest
@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_persistent_timeout_reports_and_recovers(gpu_available, oracle_mod, monkeypatch):
+def test_persistent_timeout_reports_and_recovers(gpu_available, oracle_mod):
     from ksched import MODE_BATCHED, Engine, KschedError, cluster
     cl = cluster.make_cluster("c3", n_nodes=20000, n_pods=3000)
     want = oracle_mod.schedule(cl, nthreads=8)
@@ -20,14 +20,14 @@ def test_persistent_timeout_reports_and_recovers(gpu_available, oracle_mod, monk
         e.save_state()
         e.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
 
-        monkeypatch.setenv("KSCHED_PERSIST_TIMEOUT_MS", "0")
+        e.set_timeout(0)
         with pytest.raises(KschedError) as ex:
             e.run()
             e.sync()
         msg = str(ex.value)
         assert "persistent pipeline" in msg and "timed out" in msg, msg
         assert "score batches" in msg and "commit phase" in msg, msg  # the progress words
-        monkeypatch.delenv("KSCHED_PERSIST_TIMEOUT_MS")
+        e.set_timeout(10000)
 
         def again():
             e.restore_state()
@@ -40,5 +40,4 @@ def test_persistent_timeout_reports_and_recovers(gpu_available, oracle_mod, monk
             return e.stats()["pipeline"]
 
         assert again() == "persistent"
-        monkeypatch.setenv("KSCHED_PERSIST", "0")  # the bench's fallback after a failed step
-        assert again() == "stream"
+        assert again() == "persistent"

@@ -11,10 +11,8 @@ sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd")]
 
 def run_rank(rank, world, port, cfg, nn, pp, calls, q):
     try:
-        # ranks on ONE device (test harness only; one GPU per rank in production): each score grid takes
-        # its share of the CUs, leaving enough free CUs that every rank's commit workgroup (exclusive CU)
-        # still finds one after the other ranks' mergers (up to two per free CU) have landed
-        os.environ["KSCHED_PERSIST_G"] = str(max(8, (256 - 34 * world) // world // 8 * 8))
+        # ranks on ONE device (test harness only; one GPU per rank in production): each rank's kernel takes
+        # its share of the CUs (opts.pipe_wgs, a plain launch), all of them resident at once
         os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "20000")
         import numpy as np
         import torch.distributed as dist
@@ -23,7 +21,7 @@ def run_rank(rank, world, port, cfg, nn, pp, calls, q):
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
         eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=0, mode=MODE_BATCHED, comm=False, xchg=True,
-                                            topk=16, batch=64)
+                                            topk=16, batch=64, pipe_wgs=(256 - 8) // world)
         assert eng.xchg_ready, "exchange setup failed"
         out = []
         eng.save_state()
