@@ -8,9 +8,15 @@
 // GPU; getNodes/getPods (anchor/tools.go:53-108), bind and postEvent (anchor/schedule.go:200-261,
 // anchor/tools.go:22-51) are the reference's own functions, called unchanged and in pod order.
 //
-// This file is not compiled in this repository's image (no Go toolchain); the same call sequence is
-// compiled and run against libksched.so as integration/ksched_driver.c by
-// tests/test_gpu_integration.py.  Build (with the reference checked out beside this repository):
+// This file is not compiled in this repository's image (no Go toolchain); the same call sequence --
+// create, load_nodes, schedule, explain_pod per NO_FIT pod, ordered binds, apply_delta undo of a failed
+// bind -- is compiled and run against libksched.so as integration/ksched_driver.c by
+// tests/test_gpu_integration.py.  Type-checked by inspection against the reference: NodeList.Items is
+// []*Node (anchor/types.go:99), getUnscheduledPods returns []*Pod (anchor/schedule.go:145),
+// allocatableResource / bind take *Node (anchor/predicate.go:56, anchor/schedule.go:200),
+// usedResource takes (*NodeList, *PodList) (anchor/predicate.go:83), requestedResource *Pod
+// (anchor/predicate.go:69), postEvent an Event (anchor/tools.go:22, anchor/types.go:4-40).
+// Build (with the reference checked out beside this repository):
 //
 //	CGO_CFLAGS=-I<repo>/include CGO_LDFLAGS="-L<repo>/k8s-scheduler_amd -lksched" go build -o scheduler anchor/*.go
 package main
@@ -65,7 +71,7 @@ func loadCluster(nodeList *NodeList, podList *PodList) {
 	n := len(nodeList.Items)
 	ac, am, ap := make([]int64, n), make([]int64, n), make([]int64, n)
 	for i := range nodeList.Items {
-		a := allocatableResource(&nodeList.Items[i], used) // takes *Node (anchor/predicate.go:56)
+		a := allocatableResource(nodeList.Items[i], used) // Items is []*Node (anchor/types.go:99); takes *Node (anchor/predicate.go:56)
 		ac[i], am[i], ap[i] = a.CPU, a.Memory, a.Pod
 	}
 	kschedCheck(C.ksched_load_nodes(kctx, C.int64_t(n), i64p(ac), i64p(am), i64p(ap), nil, nil), "ksched_load_nodes")
@@ -76,8 +82,11 @@ func loadCluster(nodeList *NodeList, podList *PodList) {
 func failedSchedulingEvent(pod *Pod, i int, nodeList *NodeList) {
 	var counts [C.KSCHED_NUM_REASONS]C.int64_t
 	reason := make([]uint8, len(nodeList.Items))
-	kschedCheck(C.ksched_explain_pod(kctx, C.int64_t(i), &counts[0], (*C.uint8_t)(unsafe.Pointer(&reason[0]))),
-		"ksched_explain_pod")
+	var rp *C.uint8_t // out_reason may be NULL: an empty node list has no per-node lines
+	if len(reason) > 0 {
+		rp = (*C.uint8_t)(unsafe.Pointer(&reason[0]))
+	}
+	kschedCheck(C.ksched_explain_pod(kctx, C.int64_t(i), &counts[0], rp), "ksched_explain_pod")
 	text := map[uint8]string{C.KSCHED_REASON_CPU: "Insufficient CPU",
 		C.KSCHED_REASON_MEMORY: "Insufficient Memory", C.KSCHED_REASON_POD: "Insufficient Pod"}
 	failures := make([]string, 0, len(reason))
@@ -140,7 +149,7 @@ func schedulePodsGPU() error {
 			case C.KSCHED_NO_POSITIVE_SCORE: // the reference binds a nil node here and panics
 				errPrintln(fmt.Errorf("no node scored > 0 for pod (%s)", pod.Metadata.Name), "pod schedule failed")
 			default:
-				if err := bind(pod, &nodeList.Items[idx[i]]); err != nil { // unchanged HTTP bind
+				if err := bind(pod, nodeList.Items[idx[i]]); err != nil { // unchanged HTTP bind; Items[k] is *Node (anchor/schedule.go:200)
 					errPrintln(err, "pod schedule failed")
 					var ui []int32
 					var dc, dm, dp []int64
@@ -150,8 +159,12 @@ func schedulePodsGPU() error {
 							dc, dm, dp = append(dc, rc[j]), append(dm, rm[j]), append(dp, 1)
 						}
 					}
-					kschedCheck(C.ksched_apply_delta(kctx, C.int64_t(len(ui)), (*C.int32_t)(unsafe.Pointer(&ui[0])),
-						i64p(dc), i64p(dm), i64p(dp)), "ksched_apply_delta")
+					var uip *C.int32_t // never empty here (pod i itself was placed), guarded all the same
+					if len(ui) > 0 {
+						uip = (*C.int32_t)(unsafe.Pointer(&ui[0]))
+					}
+					kschedCheck(C.ksched_apply_delta(kctx, C.int64_t(len(ui)), uip, i64p(dc), i64p(dm), i64p(dp)),
+						"ksched_apply_delta")
 					resume = i + 1
 				}
 			}

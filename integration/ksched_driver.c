@@ -6,7 +6,7 @@
  *
  *   ksched_create -> ksched_load_nodes                      (getNodes/getPods + usedResource, once)
  *   loop:  ksched_schedule(pending[start:])                 (predicate + priorities for every pod, in order)
- *          ksched_explain_batch                             (FailedScheduling lines of the NO_FIT pods,
+ *          ksched_explain_pod per NO_FIT pod, in the bind loop (FailedScheduling lines of the pod,
  *                                                            anchor/predicate.go:152-173)
  *          bind each placed pod in order                    (anchor/schedule.go:200-261)
  *          on a failed bind of pod i: the reference leaves pod i unbound and every later pod re-reads
@@ -77,7 +77,7 @@ int main(int argc, char **argv) {
     int32_t *idx = malloc(4 * p), *feas = malloc(4 * p);
     double *score = malloc(8 * p);
     int64_t *counts = calloc((size_t)p * KSCHED_NUM_REASONS, 8);
-    int64_t *call_counts = malloc((size_t)p * KSCHED_NUM_REASONS * 8);
+    uint8_t *reason = malloc((size_t)(n > 0 ? n : 1));
     int64_t calls = 0, binds = 0, failed_binds = 0, undone = 0;
     int64_t start = 0;
     while (start < p) {
@@ -86,13 +86,13 @@ int main(int argc, char **argv) {
                                 score + start, feas + start);
         if (rcode != KSCHED_OK) die(ctx, "ksched_schedule", rcode);
         ++calls;
-        int64_t nf = 0;
-        if ((rcode = ksched_explain_batch(ctx, m, call_counts, &nf)) != KSCHED_OK) die(ctx, "ksched_explain_batch", rcode);
         int64_t resume = -1;
         for (int64_t i = start; i < p; ++i) {
             if (idx[i] == KSCHED_NO_FIT) {  /* FailedScheduling event for this pod (its turn's state) */
-                memcpy(counts + i * KSCHED_NUM_REASONS, call_counts + (i - start) * KSCHED_NUM_REASONS,
-                       KSCHED_NUM_REASONS * 8);
+                /* the shim's failedSchedulingEvent: per-node reasons of pod i - start of this call */
+                if ((rcode = ksched_explain_pod(ctx, i - start, counts + i * KSCHED_NUM_REASONS, n > 0 ? reason : NULL)) !=
+                    KSCHED_OK)
+                    die(ctx, "ksched_explain_pod", rcode);
                 continue;
             }
             if (idx[i] < 0) continue; /* KSCHED_NO_POSITIVE_SCORE: the reference would panic in bind */

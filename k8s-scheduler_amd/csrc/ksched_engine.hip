@@ -563,6 +563,8 @@ void print_persist_trace(ksched_ctx *c) {
             sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
 }
 
+constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
+
 // Batched mode as ONE persistent kernel (ksched_pipe.hip): no per-batch launches, no stream events,
 // node rows in LDS.  Returns 1 (not taken) when the configuration does not fit it -- the stream pipeline
 // was asked for, multi-rank without the device exchange, a sequential commit (batch > 64), chunk lists
@@ -581,7 +583,12 @@ int enqueue_persistent(ksched_ctx *c) {
     // one workgroup per CU: the commit + G score workgroups.  At least ~96 rows per workgroup: a smaller
     // grid costs scan time but every list fewer shortens the merge (one rank's share of an 8-GPU c4,
     // 12.5k nodes: G = 128 -> 22.8 us per batch, 240 -> 23.8, 64 -> 24.6; round 2)
-    const int wgs = c->o.pipe_wgs > 0 ? std::min(c->o.pipe_wgs, c->cus) : c->cus;
+    // A launch's workgroups are dealt round-robin to the 8 XCDs (32 CUs each) and never move to another
+    // XCD: kernels of ranks that share one device each take a multiple of 8 workgroups, so no XCD is
+    // asked for more CUs than it has (82 + 82 + 82 workgroups put 33 on two XCDs: one never started)
+    const int wgs = c->o.pipe_wgs > 0 ? std::min(c->o.pipe_wgs >= kXcds ? c->o.pipe_wgs / kXcds * kXcds : c->o.pipe_wgs,
+                                                 c->cus)
+                                      : c->cus;
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1, (int64_t)kPipeMergeThreads,
                                                                (n_geom + 95) / 96}));
     if (wgs < 2) return 1;
