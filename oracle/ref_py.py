@@ -67,26 +67,75 @@ def _round_to_f32(q: Fraction) -> float:
     return sign * float(val)
 
 
-_DEC = re.compile(r"[+-]?(?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?")
+def _underscore_ok(s: str) -> bool:
+    """strconv.underscoreOK (Go atoi.go): underscores only between two digits, or between a base prefix
+    and a digit (restated from the Go language spec's digit-separator rule)."""
+    if s[:1] in ("+", "-"):
+        s = s[1:]
+    prev = "^"  # ^ start, 0 digit or base prefix, _ underscore, ! anything else
+    i = 0
+    hexd = False
+    if len(s) >= 2 and s[0] == "0" and s[1] in "bBoOxX":
+        i, prev, hexd = 2, "0", s[1] in "xX"
+    for ch in s[i:]:
+        if ch.isdigit() and ch.isascii() or (hexd and ch in "abcdefABCDEF"):
+            prev = "0"
+        elif ch == "_":
+            if prev != "0":
+                return False
+            prev = "_"
+        else:
+            if prev == "_":
+                return False
+            prev = "!"
+    return prev != "_"
+
+
+_SPECIAL = re.compile(r"([+-])?(inf|infinity)", re.IGNORECASE)
+# Go floating-point literal forms accepted by strconv.ParseFloat (digit separators checked separately):
+#   decimal  [+-] digits [. digits] [e [+-] digit {digit|_}]      (at least one mantissa digit)
+#   hex      [+-] 0x hexdigits [. hexdigits] p [+-] digit {digit|_} (the binary exponent is mandatory)
+_DEC_FORM = re.compile(r"([+-]?)([0-9_]*)(?:\.([0-9_]*))?(?:[eE]([+-]?[0-9][0-9_]*))?")
+_HEX_FORM = re.compile(r"([+-]?)0[xX]([0-9a-fA-F_]*)(?:\.([0-9a-fA-F_]*))?[pP]([+-]?[0-9][0-9_]*)")
 
 
 def go_parse_float32(s: str):
-    """strconv.ParseFloat(s, 32) for the forms the generator and tests use: decimal literals and the
-    special words.  Returns (value, err) with err in {None, "syntax", "range"}.  Hex and underscore
-    forms are only covered by the C oracle."""
-    low = s.lower()
-    body = low[1:] if low[:1] in "+-" else low
-    sign = -1.0 if low[:1] == "-" else 1.0
-    if body in ("inf", "infinity"):
-        return sign * math.inf, None
-    if low == "nan":
+    """strconv.ParseFloat(s, 32): the special words (optional sign only on the infinities), decimal and
+    hexadecimal literals with Go digit separators, correctly rounded to float32 (round half to even).
+    Returns (value, err) with err in {None, "syntax", "range"}; the value is float32-exact."""
+    m = _SPECIAL.fullmatch(s)
+    if m:
+        return (-math.inf if m.group(1) == "-" else math.inf), None
+    if s.lower() == "nan":
         return math.nan, None
-    if not _DEC.fullmatch(s):
+    hx = _HEX_FORM.fullmatch(s)
+    dc = None if hx else _DEC_FORM.fullmatch(s)
+    m = hx or dc
+    if not m or not _underscore_ok(s):
         return 0.0, "syntax"
-    v = _round_to_f32(Fraction(s))
+    sign = -1 if m.group(1) == "-" else 1
+    ip = m.group(2).replace("_", "")
+    fp = (m.group(3) or "").replace("_", "")
+    if not ip and not fp:
+        return 0.0, "syntax"  # no mantissa digit
+    ex = int(m.group(4).replace("_", "")) if m.group(4) else 0
+    base = 16 if hx else 10
+    mant = int(ip + fp, base) if ip + fp else 0
+    if mant == 0:
+        return (-0.0 if sign < 0 else 0.0), None
+    if hx:
+        q = Fraction(mant) * Fraction(2) ** (ex - 4 * len(fp))
+    else:
+        mag = len(str(mant)) + ex - len(fp)  # decimal digits of the integer part
+        if mag > 40:                          # beyond float32's range: +-Inf, ErrRange
+            return sign * math.inf, "range"
+        if mag < -60:                         # below half the smallest subnormal: +-0
+            return (-0.0 if sign < 0 else 0.0), None
+        q = Fraction(mant) * Fraction(10) ** (ex - len(fp))
+    v = _round_to_f32(q)
     if math.isinf(v):
-        return v, "range"
-    return v, None
+        return sign * v, "range"
+    return sign * v, None
 
 
 def go_f64_to_i64(x: float) -> int:

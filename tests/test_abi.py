@@ -75,6 +75,31 @@ def test_product_parser_matches_oracle_random(oracle_mod):
                 assert rc == L.E_PARSE, (kind, s)
 
 
+def test_product_parser_matches_independent_python_random():
+    """The product parser (csrc/packer.cpp) against the pure-Python restatement of Go's strconv
+    (oracle/ref_py.py: its own ParseFloat32 with hex literals and digit separators, written from the Go
+    spec rather than from the C code) on random strings of the literal grammar's alphabet."""
+    import ctypes as C
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_py as R
+    from ksched import _lib as L
+    rng = np.random.default_rng(11)
+    pieces = ["0", "1", "7", "9", "0x", "0X", ".", "e", "E", "p", "P", "+", "-", "_", "a", "f", "F", "inf", "nan",
+              "Infinity", "m", "Ki", "Mi", "5", "3"]
+    pyf = {"cpu": R.parse_cpu, "memory": R.parse_memory, "pods": R.parse_pods}
+    for _ in range(6000):
+        s = "".join(rng.choice(pieces, size=int(rng.integers(1, 7))))
+        for kind in ("cpu", "memory", "pods"):
+            out = C.c_int64(0)
+            rc = getattr(L.lib(), f"ksched_parse_{kind}")(s.encode(), C.byref(out))
+            try:
+                want = pyf[kind](s)
+                assert rc == L.OK and out.value == want, (kind, s, out.value, want)
+            except R.Fatal:
+                assert rc == L.E_PARSE, (kind, s)
+
+
 def test_price_parse():
     from ksched.host import FatalParse, parse_price
     assert parse_price("0.05") == np.float32(0.05)

@@ -23,7 +23,7 @@ import os
 import sys
 from collections import defaultdict
 
-FAMILIES = {"k_persist_score": "score", "k_persist_merge": "merge", "k_persist_commit": "commit",
+FAMILIES = {"k_pipe": "pipe", "k_persist_score": "score", "k_persist_merge": "merge", "k_persist_commit": "commit",
             "k_score_topk": "score", "k_merge_pod": "merge", "k_merge": "merge", "k_commit": "commit",
             "k_exact": "exact"}
 CUS = 256
@@ -76,6 +76,10 @@ def main():
                 k["fp64_issue_frac"] = 4 * f64 / cyc
                 if "SQ_INSTS_VALU" in avg:  # from the same run only when both groups were in one pass
                     k["valu_busy_frac"] = (4 * f64 + 2 * (avg["SQ_INSTS_VALU"] - f64)) / cyc
+            if "SQ_ACTIVE_INST_VALU" in avg:  # quad-cycles in which a wave issued VALU, summed over waves
+                k["active_inst_valu_frac"] = 4 * avg["SQ_ACTIVE_INST_VALU"] / cyc
+            if "SQ_BUSY_CYCLES" in avg:
+                k["sq_busy_cycles_per_launch"] = avg["SQ_BUSY_CYCLES"]
         res["kernels"][kern] = k
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
