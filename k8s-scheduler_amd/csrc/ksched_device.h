@@ -44,8 +44,9 @@ struct alignas(16) NodeRec {
     uint64_t labels;   // label bitset (build extension)
     double af[3];      // (double)a[k], kept in sync with a[k] by every writer (device side)
     double y[3];       // recip(af[k]): hipcc's refined reciprocal of the divisor (0 when a[k] == 0)
+    float ys[3];       // screen_recip(a[k]): f32 reciprocal for the screened scan (maintained in the
+                       // persistent pipeline's LDS rows only; stale in HBM)
     float price;       // node price (best-price priority)
-    uint32_t pad[3];
 };
 static_assert(sizeof(NodeRec) == 96, "NodeRec layout");
 // The same rows seen through the constant address space: wave-uniform reads become scalar loads.
@@ -228,6 +229,41 @@ __device__ __forceinline__ bool pair_key_fast(bool feas, int64_t rc, int64_t rm,
 }
 
 __device__ __forceinline__ double recip_or_zero(int64_t a, double af) { return a == 0 ? 0.0 : recip(af); }
+
+// ---- f32 screen of the resource score (the persistent pipeline's screened scan) ----
+// For a FITTING pair (0 <= r_k <= a_k, 0 < a_k < 2^52) with fractions f_k = r_k / a_k the reference score
+// (anchor/priorities.go:5-23,45-50) is, in real arithmetic and when every f_k < 1,
+//     s = ((1 - var) * 10 + 10 (1 - mu)) / 2 = 10 - (5/3) S - (5/3) Q + (5/9) S^2,
+//     S = f_c + f_m + f_p,  Q = f_c^2 + f_m^2 + f_p^2   (mu = S / 3, var = Q / 3 - mu^2),
+// and s = 5 (1 - mu) <= that polynomial when some f_k == 1 (the balanced part is then 0, anchor/
+// priorities.go:10-12).  screen_score evaluates the polynomial in f32 from f32 requests and f32
+// reciprocals.  Its error against the f64 score of the reference's operation order is below 1.3e-5
+// (f_k relative error <= 3u, u = 2^-24; S <= 15u, Q <= 30u, S^2 <= 100u absolute; the final combination
+// of values <= 10 adds <= 80u; the f64 score is within 1e-14 of the real one): kScreenEps = 1e-4 leaves a
+// 7x margin (tests/test_screen_bound.py checks it on random and adversarial pairs).  A screen never
+// decides a result: it only proves that a pair cannot enter a workgroup's top-KC list, and every pair
+// it cannot exclude is scored exactly.
+constexpr float kScreenEps = 1e-4f;
+constexpr float kScreenNoFitHi = 10.0f / 3.0f + 1e-4f;  // bound of a NON-fitting pair's score (DomAll):
+                                                         // balanced 0, at most two least terms of 10 -> 20/3/2
+// 1/a in f32 for 0 < a < 2^52; NaN otherwise (every pair with this node is then scored exactly)
+__host__ __device__ __forceinline__ float screen_recip(int64_t a) {
+    return (a > 0 && a < (1ll << 52)) ? (float)(1.0 / (double)a) : __builtin_nanf("");
+}
+// a request in f32; NaN when negative or >= 2^52 (scored exactly)
+__host__ __device__ __forceinline__ float screen_req(int64_t r) {
+    return (r >= 0 && r < (1ll << 52)) ? (float)r : __builtin_nanf("");
+}
+// the polynomial above (NaN propagates: callers treat a NaN screen as "score exactly"); *fmax = the
+// largest f32 fraction (a fraction near 1 may hide a zero balanced part)
+__device__ __forceinline__ float screen_score(float rc, float rm, float rp, float yc, float ym, float yp,
+                                              float *fmax) {
+    const float c = rc * yc, m = rm * ym, p = rp * yp;
+    *fmax = __builtin_fmaxf(__builtin_fmaxf(c, m), p);
+    const float S = (c + m) + p;
+    const float Q = (c * c + m * m) + p * p;
+    return ((10.0f - (5.0f / 3.0f) * S) - (5.0f / 3.0f) * Q) + (5.0f / 9.0f) * (S * S);
+}
 
 // Upper bound of the resource score without the division corrections: every a / b is replaced by
 // a * recip(b) (relative error <= 2^-51 per quotient), so |approx - exact| <= ~1e3 * 2^-52 *

@@ -974,7 +974,7 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
         r.y[0] = r.y[1] = r.y[2] = 0.0;
         r.labels = labels ? labels[i] : 0;
         r.price = (price && price[i] != 0.f) ? price[i] : 0.f;  // "-0" == "0": canonical +0 (price_key)
-        r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        r.ys[0] = r.ys[1] = r.ys[2] = 0.f;
         mx = std::max(mx, std::max(uabs(ac[i]), std::max(uabs(am[i]), uabs(ap[i]))));
         if (price && !std::isfinite(price[i])) return fail(c, KSCHED_E_INVALID, "load_nodes: non-finite price");
     }

@@ -58,7 +58,9 @@ struct alignas(16) PipeCtl {
     int32_t s_stop, m_stop;
     int64_t s_p0, s_done;         // score role: this batch's plan and the cursor after commit(b-2)
     int64_t m_p0, m_done;         // merge role: the same, read by its own poll
-    int32_t c_stop, pad;          // commit workgroup
+    int32_t c_stop;               // commit workgroup
+    int32_t s_ex;                 // score role: rows of this batch scored exactly (screened scan)
+    int32_t s_scr;                // score role: this batch uses the screened scan
 };
 constexpr size_t kPipeCtlBytes = 64;
 static_assert(sizeof(PipeCtl) <= kPipeCtlBytes, "PipeCtl");
@@ -157,6 +159,29 @@ __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int
     const double f0 = (double)a0, f1 = (double)a1, f2 = (double)a2;
     nd->af[0] = f0; nd->af[1] = f1; nd->af[2] = f2;
     nd->y[0] = recip_or_zero(a0, f0); nd->y[1] = recip_or_zero(a1, f1); nd->y[2] = recip_or_zero(a2, f2);
+    nd->ys[0] = screen_recip(a0); nd->ys[1] = screen_recip(a1); nd->ys[2] = screen_recip(a2);
+}
+
+// t (sorted descending) <- the KC largest of t and u (both sorted descending): the element-wise max of t
+// and reversed u holds them as a bitonic sequence, which half-cleaners sort
+template <int KC>
+__device__ __forceinline__ void topk_merge_u32(uint32_t (&t)[KC], const uint32_t (&u)[KC]) {
+    uint32_t v[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) v[q] = t[q] > u[KC - 1 - q] ? t[q] : u[KC - 1 - q];
+#pragma unroll
+    for (int d = KC / 2; d >= 1; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+            if ((i & d) == 0) {
+                const uint32_t a = v[i], b = v[i + d];
+                v[i] = a > b ? a : b;
+                v[i + d] = a > b ? b : a;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) t[q] = v[q];
 }
 
 // LDS layout of a score workgroup: PipeCtl | rows [R] | fold lists | merge scratch | exchange messages
@@ -204,7 +229,18 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (j < n) reinterpret_cast<int4 *>(rows + r)[piece] = reinterpret_cast<const int4 *>(P.nodes + j)[piece];
     }
     sync();
+    for (int r = tid; r < R; r += kST) {  // the screen's f32 reciprocals (LDS rows only)
+        NodeRec &nd = rows[r];
+        nd.ys[0] = screen_recip(nd.a[0]); nd.ys[1] = screen_recip(nd.a[1]); nd.ys[2] = screen_recip(nd.a[2]);
+    }
+    // (batch 0's first barrier orders these writes before any export apply or scan)
     const double y3 = recip(3.0);
+    // The screened scan (resource priority with the FAST53 bound): a row is scored exactly only when, for
+    // some pod of the batch, its f32 screen cannot prove the pair below the workgroup's KC-th best key;
+    // each workgroup turns it off for a while when most of its rows need the exact score anyway
+    constexpr bool kScreen = PRIO == kPrioResource && F53;
+    constexpr int kScreenOffBatches = 16;
+    int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
     int64_t nact = 0;
     int idle = 0;
     for (int64_t b = 0;; ++b) {
@@ -259,6 +295,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 pc->s_p0 = p0v;
                 pc->s_done = donev;
                 pc->s_stop = errv != 0 ? 3 : stop;
+                pc->s_scr = kScreen && b >= scr_off_until;
+                pc->s_ex = 0;
             }
         }
         sync();
@@ -296,6 +334,108 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
 #pragma unroll
         for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
         int32_t cnt = 0;
+        auto insert = [&](double ck, int32_t ci) {
+            bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+                const bool sw = moved || ck > key[q];
+                moved = sw;
+                const double tk = key[q];
+                const int32_t ti = idx[q];
+                key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
+                ck = sw ? tk : ck; ci = sw ? ti : ci;
+            }
+        };
+        const bool scr = kScreen && pc->s_scr;  // workgroup-uniform
+        if (scr) {
+            // Bounds travel shifted by +1 as f32 bit patterns: every one is then 0 ("none") or a positive
+            // float, whose bits order as unsigned integers (max/min without NaN canonicalisation).
+            const float qc = screen_req(rc), qm = screen_req(rm), qp = screen_req(rp);
+            auto screen = [&](const NodeRec &nd, bool *f, float *s, float *fm) {
+                *f = fits(rc, rm, rp, sel, nd.a[0], nd.a[1], nd.a[2], nd.labels, LAB);
+                *s = screen_score(qc, qm, qp, nd.ys[0], nd.ys[1], nd.ys[2], fm);
+            };
+            // ---- pass 1: every row -- the predicate count, and the KC largest lower bounds (screen - eps)
+            // of the pairs that surely carry an eligible key ----
+            uint32_t t[KC];
+#pragma unroll
+            for (int q = 0; q < KC; ++q) t[q] = 0u;
+            for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
+                uint32_t xs[kPU];
+#pragma unroll
+                for (int u = 0; u < kPU; ++u) {
+                    const int r = r0 + u * kSW;
+                    xs[u] = 0u;
+                    if (r < R && g + (int64_t)r * G < n) {  // wave-uniform
+                        bool f;
+                        float sc, fm;
+                        screen(rows[r], &f, &sc, &fm);
+                        cnt += f;
+                        // a fraction near 1 may zero the balanced part; NaN (unscreenable) fails every test
+                        const bool lo_ok = active && f && fm < 0.999f && sc > 0.0f;
+                        xs[u] = lo_ok ? __float_as_uint(sc + (1.0f - kScreenEps)) : 0u;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kPU; ++u) {
+                    uint32_t x = xs[u];
+#pragma unroll
+                    for (int q = 0; q < KC; ++q) {
+                        const uint32_t hi = t[q] > x ? t[q] : x;
+                        x = t[q] > x ? x : t[q];
+                        t[q] = hi;
+                    }
+                }
+            }
+            // ---- the workgroup's bound: the KC-th largest lower bound over every wave's list (the fold
+            // area is free until the scan ends) ----
+            uint32_t *sl = reinterpret_cast<uint32_t *>(fold);  // [kSW][KC][64]
+#pragma unroll
+            for (int q = 0; q < KC; ++q) sl[(wave * KC + q) * 64 + lane] = t[q];
+            sync();
+            for (int w = 1; w < kSW; ++w) {
+                const int ow = (wave + w) & (kSW - 1);
+                uint32_t u[KC];
+#pragma unroll
+                for (int q = 0; q < KC; ++q) u[q] = sl[(ow * KC + q) * 64 + lane];
+                topk_merge_u32<KC>(t, u);
+            }
+            const float L = __uint_as_float(t[KC - 1]);  // + 1; 0 = fewer than KC bounds: everything passes
+            // ---- pass 2: a row is scored exactly (for every pod) when some pod's screen cannot prove its
+            // pair below L; a pair below L is below KC eligible keys of this workgroup, so it is in no
+            // top-KC list the exact scan would have produced ----
+            int nex = 0;
+            for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
+                bool need[kPU], fs[kPU];
+#pragma unroll
+                for (int u = 0; u < kPU; ++u) {
+                    const int r = r0 + u * kSW;
+                    need[u] = false;
+                    fs[u] = false;
+                    if (r < R && g + (int64_t)r * G < n) {
+                        float sc, fm;
+                        screen(rows[r], &fs[u], &sc, &fm);
+                        const float hi = fs[u] ? sc + (1.0f + kScreenEps) : (DOM == kDomAll ? kScreenNoFitHi + 1.0f : 0.0f);
+                        need[u] = active && (DOM == kDomAll || fs[u]) && !(hi < L);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kPU; ++u) {
+                    if (__ballot(need[u])) {  // wave-uniform; rows in ascending node order
+                        ++nex;
+                        const int r = r0 + u * kSW;
+                        const NodeRec &nd = rows[r];
+                        const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+                        double k;
+                        const bool el = pair_key_fast<PRIO, DOM, F53>(fs[u], rc, rm, rp, rcf, rmf, rpf, ac, am, ap,
+                                                                      nd.af[0], nd.af[1], nd.af[2], nd.y[0], nd.y[1],
+                                                                      nd.y[2], y3, nd.price, &k);
+                        insert(el ? k : -__builtin_inf(), (int32_t)(P.node_offset + g + (int64_t)r * G));
+                    }
+                }
+            }
+            if (nex && lane == 0) atomicAdd(&pc->s_ex, nex);
+        } else
         // kPU rows per step: their keys are independent f64 chains the scheduler interleaves; inserted
         // in ascending node order afterwards
         for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
@@ -365,6 +505,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
         int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
         if (wave == 0) {
+            // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
+            if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
             // s_cnt: every wave added before the last fold barrier
             if (active) {
                 Cand *dst = part + ((size_t)lane * G + g) * KC;

@@ -60,3 +60,28 @@ def test_full_size_c5_high_conflict(gpu_available, oracle_mod):
     a, b = full_check(cl, oracle_mod, 20000, dict(topk=16, batch=64))
     st = b[4]
     assert st["truncations"] > 0.1 * st["batches"], st
+
+
+@pytest.mark.parametrize("mode", ["exact", "batched"])
+def test_full_size_c2(gpu_available, oracle_mod, mode):
+    """BASELINE config 2 at full size (10k pods x 5k nodes, best-price, feasible-only): every pod against
+    the oracle (5e7 pairs), in the sequential exact mode the config names and in the batched pipeline."""
+    from ksched import MODE_BATCHED, MODE_EXACT, cluster
+    cl = cluster.make_cluster("c2")
+    assert (cl.n_pods, cl.n_nodes) == (10_000, 5_000)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    if mode == "exact":
+        got = run_engine(cl, MODE_EXACT)
+    else:
+        got = run_engine(cl, MODE_BATCHED, topk=16, batch=64)
+    assert_same(got, want, f"c2 full {mode}")
+    assert got[4]["pipeline"] == ("exact" if mode == "exact" else "persistent")
+
+
+def test_full_size_c3_all_pods_vs_oracle(gpu_available, oracle_mod):
+    """BASELINE config 3 (100k pods x 50k nodes) through the batched pipeline, every pod against the oracle
+    (5e9 pairs, OpenMP)."""
+    from ksched import MODE_BATCHED, cluster
+    cl = cluster.make_cluster("c3")
+    want = oracle_mod.schedule(cl, nthreads=16)
+    assert_same(run_engine(cl, MODE_BATCHED, topk=16, batch=64), want, "c3 full batched vs oracle")

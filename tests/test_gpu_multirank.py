@@ -73,6 +73,20 @@ def test_rank_group_equals_sequential(gpu_available, oracle_mod, R, case):
     assert len({(o[4]["batches"], o[4]["truncations"], o[4]["placed"]) for o in out}) == 1
 
 
+@pytest.mark.parametrize("R", [2, 8])
+def test_rank_group_c4_full_nodes(gpu_available, oracle_mod, R):
+    """c4 node-sharded at the FULL 100k nodes (R = 2: 50k per rank; R = 8: the 8-GPU split, 12.5k per rank),
+    a 5k-pod prefix against the sequential oracle, final state included."""
+    from ksched import cluster
+    cl = cluster.make_cluster("c4", n_pods=5000)
+    assert cl.n_nodes == 100_000
+    want = oracle_mod.schedule(cl, nthreads=16)
+    out, final = run_group(cl, R, topk=16, batch=64)
+    for r in range(R):
+        assert_same(out[r][:3] + ((),), want, f"c4 R={R} rank {r}")
+    assert_same((want[0], want[1], want[2], final), want, f"c4 R={R} final state")
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_rank_group_edge_clusters(gpu_available, oracle_mod, seed):
     """Adversarial small clusters (negative / zero allocatable, 2^53+ values, ties, labels, best price)

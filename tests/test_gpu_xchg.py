@@ -25,7 +25,8 @@ def _port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,nn,pp,world", [("c3", 24000, 3000, 2), ("c5hc", 20000, 3000, 2), ("c4", 30000, 2500, 3)])
+@pytest.mark.parametrize("cfg,nn,pp,world", [("c3", 24000, 3000, 2), ("c5hc", 20000, 3000, 2), ("c4", 30000, 2500, 3),
+                                                     ("c4", 100000, 2500, 2)])
 def test_xchg_ranks_match_oracle(cfg, nn, pp, world):
     import oracle as O
     import xchg_worker

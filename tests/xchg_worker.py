@@ -11,8 +11,11 @@ sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd")]
 
 def run_rank(rank, world, port, cfg, nn, pp, calls, q):
     try:
-        # ranks on ONE device (test harness only; one GPU per rank in production): each rank's kernel takes
-        # its share of the CUs (opts.pipe_wgs, a plain launch), all of them resident at once
+        # ranks on ONE device (test harness only; one GPU per rank in production): each rank's kernel is a
+        # plain launch of opts.pipe_wgs workgroups, one CU each, and the ranks wait on one another, so they
+        # must all be resident at once -- which nothing guarantees for independent launches of separate
+        # processes.  Half the CUs in total leaves every XCD room for an uneven placement (at 3 x 80 of 256
+        # a rank once started only after the others' waits expired)
         os.environ.setdefault("KSCHED_PERSIST_TIMEOUT_MS", "20000")
         import numpy as np
         import torch.distributed as dist
@@ -21,7 +24,7 @@ def run_rank(rank, world, port, cfg, nn, pp, calls, q):
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
         eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=0, mode=MODE_BATCHED, comm=False, xchg=True,
-                                            topk=16, batch=64, pipe_wgs=(256 - 8) // world)
+                                            topk=16, batch=64, pipe_wgs=128 // world)
         assert eng.xchg_ready, "exchange setup failed"
         out = []
         eng.save_state()
