@@ -230,22 +230,23 @@ __device__ __forceinline__ bool pair_key_fast(bool feas, int64_t rc, int64_t rm,
 
 __device__ __forceinline__ double recip_or_zero(int64_t a, double af) { return a == 0 ? 0.0 : recip(af); }
 
-// ---- f32 screen of the resource score (the persistent pipeline's screened scan, DESIGN.md section 4.2) ----
-// For a FITTING pair (0 <= r_k <= a_k, 0 < a_k < 2^52) with fractions f_k = r_k / a_k the reference score
-// (anchor/priorities.go:5-23,45-50) is, in real arithmetic and when every f_k < 1,
+// ---- f32 screen of the resource score (the persistent pipeline's screened scan, DESIGN.md section 4.1) ----
+// With fractions f_k = r_k / a_k (0 < a_k < 2^52, 0 <= r_k < 2^52) the reference score (anchor/priorities.go:
+// 5-23,45-50) is, in real arithmetic,
+//   resource-fitting pair (every r_k <= a_k), every f_k < 1:
 //     s = ((1 - var) * 10 + 10 (1 - mu)) / 2 = 10 - (5/3) S - (5/3) Q + (5/9) S^2,
-//     S = f_c + f_m + f_p,  Q = f_c^2 + f_m^2 + f_p^2   (mu = S / 3, var = Q / 3 - mu^2),
-// and s = 5 (1 - mu) <= that polynomial when some f_k == 1 (the balanced part is then 0, anchor/
-// priorities.go:10-12).  screen_score evaluates the polynomial in f32 from f32 requests and f32
-// reciprocals.  Its error against the f64 score of the reference's operation order is below 1.3e-5
-// (f_k relative error <= 3u, u = 2^-24; S <= 15u, Q <= 30u, S^2 <= 100u absolute; the final combination
-// of values <= 10 adds <= 80u; the f64 score is within 1e-14 of the real one): kScreenEps = 1e-4 leaves a
-// 7x margin (tests/test_screen_bound.py checks it on random and adversarial pairs).  A screen never
-// decides a result: it only proves that a pair cannot enter a workgroup's top-KC list, and every pair
-// it cannot exclude is scored exactly.
-constexpr float kScreenEps = 1e-4f;
-constexpr float kScreenNoFitHi = 10.0f / 3.0f + 1e-4f;  // bound of a NON-fitting pair's score (DomAll):
-                                                         // balanced 0, at most two least terms of 10 -> 20/3/2
+//     S = f_c + f_m + f_p,  Q = f_c^2 + f_m^2 + f_p^2      (mu = S / 3, var = Q / 3 - mu^2);
+//   some f_k == 1 exactly: the balanced part is 0 (priorities.go:10-12) and s = 5 (1 - mu) <= the polynomial;
+//   some r_k > a_k: balanced part 0, that resource's least-requested term 0 (scores.go:21), so
+//     s = (5/3) * sum over the k with r_k <= a_k of (1 - f_k).
+// screen_pair evaluates the applicable form in f32 from f32 requests and f32 reciprocals.  Error against the
+// f64 score of the reference's operation order: < 1.3e-5 for the polynomial (f_k relative error <= 3u,
+// u = 2^-24; S <= 15u, Q <= 30u, S^2 <= 100u absolute; the final combination of values <= 10 adds <= 80u;
+// the f64 score is within 1e-14 of the real one), < 2e-6 for the non-fitting form.  kScreenEps = 4e-5 keeps
+// a 3x margin (tests/test_screen_bound.py checks both forms on random, adversarial and c4-like pairs).  A screen
+// never decides a result: it only proves that a pair cannot enter a workgroup's top-KC list; every pair it
+// cannot exclude is scored exactly.
+constexpr float kScreenEps = 4e-5f;
 // 1/a in f32 for 0 < a < 2^52; NaN otherwise (every pair with this node is then scored exactly)
 __host__ __device__ __forceinline__ float screen_recip(int64_t a) {
     return (a > 0 && a < (1ll << 52)) ? (float)(1.0 / (double)a) : __builtin_nanf("");
@@ -254,15 +255,26 @@ __host__ __device__ __forceinline__ float screen_recip(int64_t a) {
 __host__ __device__ __forceinline__ float screen_req(int64_t r) {
     return (r >= 0 && r < (1ll << 52)) ? (float)r : __builtin_nanf("");
 }
-// the polynomial above (NaN propagates: callers treat a NaN screen as "score exactly"); *fmax = the
-// largest f32 fraction (a fraction near 1 may hide a zero balanced part)
-__device__ __forceinline__ float screen_score(float rc, float rm, float rp, float yc, float ym, float yp,
-                                              float *fmax) {
-    const float c = rc * yc, m = rm * ym, p = rp * yp;
-    *fmax = __builtin_fmaxf(__builtin_fmaxf(c, m), p);
+// The screen of one pair.  ok* = (a_k >= r_k) per resource (exact int64 compares).  Returns the f32 value
+// (NaN: unscreenable, every comparison then asks for the exact score); *lo_ok: the pair surely carries an
+// eligible key >= value - eps (its value may serve as a lower bound: a polynomial pair with a fraction near 1
+// may have lost its balanced part, so it never does).
+__device__ __forceinline__ float screen_pair(float qc, float qm, float qp, float yc, float ym, float yp, bool okc,
+                                             bool okm, bool okp, bool *lo_ok) {
+    const float c = qc * yc, m = qm * ym, p = qp * yp;
+    const bool rf = okc & okm & okp;
+    const float fmax = __builtin_fmaxf(__builtin_fmaxf(c, m), p);
     const float S = (c + m) + p;
     const float Q = (c * c + m * m) + p * p;
-    return ((10.0f - (5.0f / 3.0f) * S) - (5.0f / 3.0f) * Q) + (5.0f / 9.0f) * (S * S);
+    const float poly = ((10.0f - (5.0f / 3.0f) * S) - (5.0f / 3.0f) * Q) + (5.0f / 9.0f) * (S * S);
+    // any unscreenable input (S is NaN) makes the value NaN in both forms (0 * S: no branch; S is finite
+    // otherwise): the non-fitting form drops a resource's term only when its request exceeds a POSITIVE
+    // allocatable (fraction > 1)
+    const float nf = (5.0f / 3.0f) * (((okc ? 1.0f - c : 0.0f) + (okm ? 1.0f - m : 0.0f)) + (okp ? 1.0f - p : 0.0f)) +
+                     0.0f * S;
+    const float v = rf ? poly : nf;
+    *lo_ok = (rf ? fmax < 0.999f : true) && v > kScreenEps;  // false for NaN
+    return v;
 }
 
 // Upper bound of the resource score without the division corrections: every a / b is replaced by

@@ -118,7 +118,7 @@ struct ksched_ctx {
     // persistent single-rank pipeline (ksched_persist.hip)
     void *d_pws = nullptr;       // per-workgroup part lists + counts
     uint64_t *d_prog = nullptr;   // persistent pipeline: per-workgroup progress words (in d_pws)
-    int prog_G = 0, prog_B = 0;
+    int prog_G = 0, prog_B = 0, prog_rows = 0;
     uint64_t *d_trace = nullptr;  // KSCHED_PERSIST_TRACE: per-batch wall-clock stamps
     int64_t trace_cap = 0;
     size_t pws_bytes = 0;
@@ -140,6 +140,7 @@ struct ksched_ctx {
     //   KSCHED_DEBUG=1           launch decisions to stderr
     struct {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
+        bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
     } diag;
 };
@@ -514,6 +515,8 @@ void print_persist_trace(ksched_ctx *c) {
     if (hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
     double sum[14] = {};
+    double scr[5] = {};  // WG 0 wave 0, screened batches: pass 1, bound merge, pass 2, exact phase (sums), exact rows
+    int64_t nscr = 0;
     int64_t cnt = 0, first = -1, last = -1;
     for (int64_t b = 2; b < c->trace_cap; ++b) {
         if (!at(b, 0) || !at(b, 1) || !at(b, 2) || !at(b, 3) || !at(b, 4) || !at(b - 2, 4)) continue;
@@ -534,6 +537,14 @@ void print_persist_trace(ksched_ctx *c) {
         sum[11] += (double)(int64_t)(at(b, 9) - at(b, 8));     // WG 0: waiting for its slowest wave
         sum[12] += (double)(int64_t)(at(b, 10) - at(b, 9));    // WG 0: fold
         sum[13] += (double)(int64_t)(at(b, 5) - at(b, 10));    // WG 0: list stores + drain
+        if (at(b, 11) && at(b, 12)) {  // a screened batch (ksched_pipe.hip score_role)
+            ++nscr;
+            scr[0] += (double)(int64_t)(at(b, 11) - at(b, 0));
+            scr[1] += (double)(int64_t)(at(b, 12) - at(b, 11));
+            scr[2] += (double)(int64_t)(at(b, 14) - at(b, 12));
+            scr[3] += (double)(int64_t)(at(b, 8) - at(b, 14));
+            scr[4] += (double)at(b, 13);
+        }
     }
     if (c->d_dbg) {
         int64_t hd[16];
@@ -561,6 +572,11 @@ void print_persist_trace(ksched_ctx *c) {
             (long long)cnt, 0.01 * (double)(int64_t)(at(last, 4) - at(first, 4)) / (double)std::max<int64_t>(1, last - first),
             sum[0] * us, sum[1] * us, sum[2] * us, sum[3] * us, sum[4] * us, sum[5] * us, sum[6] * us, sum[7] * us,
             sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
+    if (nscr)
+        fprintf(stderr, "persist screen (WG 0 wave 0): %lld of %lld batches screened | pass 1 %.2f us, bound %.2f us, "
+                "pass 2 %.2f us, exact rows %.2f us (%.2f of the workgroup's %d rows)\n", (long long)nscr, (long long)cnt,
+                0.01 * scr[0] / nscr, 0.01 * scr[1] / nscr, 0.01 * scr[2] / nscr, 0.01 * scr[3] / nscr, scr[4] / nscr,
+                c->prog_rows);
 }
 
 constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
@@ -634,6 +650,7 @@ int enqueue_persistent(ksched_ctx *c) {
     a.prog = reinterpret_cast<uint64_t *>(a.xring + 5 * xb);
     c->d_prog = a.prog;
     c->prog_G = G;
+    c->prog_rows = R;
     c->prog_B = B;
     a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
     fill_xchg_args(c, &a);
@@ -641,6 +658,7 @@ int enqueue_persistent(ksched_ctx *c) {
     // every wait is bounded: 10 s of the 100 MHz wall clock by default (a profiler that suspends the
     // queues for a while must not turn into a spurious timeout)
     a.timeout_ticks = c->diag.persist_timeout_ms * 100000;
+    a.no_screen = c->diag.no_screen ? 1 : 0;
     if (c->diag.trace) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {
@@ -774,6 +792,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.commit_stamps = env_int("KSCHED_COMMIT_STAMPS", 0) != 0;
     c->diag.merge_stamps = env_int("KSCHED_MERGE_STAMPS", 0) != 0;
     c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
+    c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane

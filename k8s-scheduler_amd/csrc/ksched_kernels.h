@@ -357,6 +357,7 @@ struct PersistArgs {
     OutArgs out;
     int32_t *err;           // device error word (5..9 = a persistent wait timed out)
     int64_t timeout_ticks;
+    int32_t no_screen;      // diagnostics (KSCHED_NO_SCREEN): the exact scan in every batch
     // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
     uint64_t *trace;
     int64_t trace_cap;

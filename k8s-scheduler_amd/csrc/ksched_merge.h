@@ -247,4 +247,192 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b, 
 }
 
 
+
+// ------------------------------------------------------------------------------------------------
+// The same merge for the persistent pipeline's merge waves (MT = 256: W = 4 waves, one list per thread),
+// with ONE barrier and no LDS-latency-bound loops: every rank is counted over register broadcasts
+// (v_readlane of all 64 lanes) instead of LDS reads.
+//   A. (every wave) rank each list head among the wave's 64 heads; the K best go to LDS;
+//   B. (wave 0, lane = one of the W*K <= 64 survivors) rank the survivors; the K best heads' lists are kept;
+//   C. (wave 0, lane = one or two of the kept lists' K*KC entries) rank the entries; rank < K is the
+//      output position.  Then the exact-prefix cut and the Rec rows as in merge_pod_body.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// how many lanes of this wave hold a (code, idx) better than (mc, mi) -- (code, idx) pairs are distinct
+__device__ __forceinline__ int wave_rank(uint64_t code, int32_t idx, uint64_t mc, int32_t mi) {
+    int r = 0;
+#pragma unroll
+    for (int l = 0; l < 64; ++l)
+        r += code_better(readlane_u64(code, l), __builtin_amdgcn_readlane(idx, l), mc, mi) ? 1 : 0;
+    return r;
+}
+
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int KC, int K, bool COH, int MT, typename Sync>
+__device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, const int tid, MergeSmem<KC, K, MT> &sm,
+                                               Sync sync) {
+    __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
+    constexpr int W = MT / 64;
+    static_assert(W * K <= 64, "survivors must fit one wave");
+    constexpr int E = K * KC;              // the kept lists' entries
+    constexpr int EP = (E + 63) / 64;      // entries per lane
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const bool dbg = A.dbg != nullptr;
+    uint64_t ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
+    const int64_t p0 = A.p0_known ? A.p0v : load_i64<COH>(A.cursor);
+    if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // uniform over the merging threads
+    const bool has = tid < A.C_in;
+    uint64_t code[KC];
+    int32_t idx[KC];
+    int n = 0;
+    int64_t cnt = 0;
+    {
+        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? tid : 0)) * KC;
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            int32_t x;
+            double kq;
+            if (COH) {
+                x = has ? (int32_t)(uint32_t)ld_coh(&src[q].idx) : kNoIdx;
+                kq = has ? ld_coh_f64(&src[q].key) : 0.0;
+            } else {
+                x = has ? src[q].idx : kNoIdx;
+                kq = has ? src[q].key : 0.0;
+            }
+            idx[q] = x;
+            code[q] = x == kNoIdx ? 0ull : key_code(kq);
+            n += x != kNoIdx;
+        }
+        if (has) cnt = load_i64<COH>(A.in_cnt + (size_t)b * A.C_in + tid);
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { sm.code[tid][q] = code[q]; sm.idx[tid][q] = idx[q]; }
+    if (lane < K) { sm.ccode[wave * K + lane] = 0ull; sm.cidx[wave * K + lane] = kNoIdx; }  // before this wave's survivors
+    if (dbg) { asm volatile("" ::"v"(code[0]), "v"(cnt)); ts[1] = __builtin_amdgcn_s_memtime(); }
+    {   // wave partials: best cutoff (last entry of a full list), count, cut flag, valid heads
+        const bool cut = n == KC;
+        const uint64_t ck = cut ? code[KC - 1] : 0ull;
+        const int32_t ci = cut ? idx[KC - 1] : kNoIdx;
+        const uint64_t bc = wave_max_u64(ck);
+        const int32_t bi = wave_min_i32((ck == bc && ci != kNoIdx) ? ci : kNoIdx);
+        const int64_t wc = wave_sum_i64(cnt);
+        const bool wcut = __ballot(cut) != 0;
+        const int nv = __popcll(__ballot(idx[0] != kNoIdx));
+        if (lane == 0) { sm.wck[wave] = bc; sm.wci[wave] = bi; sm.wcut[wave] = wcut; sm.wcnt[wave] = wc; sm.wnv[wave] = nv; }
+    }
+    // A. rank each head within its wave
+    {
+        const int rk = wave_rank(code[0], idx[0], code[0], idx[0]);
+        wave_lds_order();  // the slot initialisation above precedes every survivor write of this wave
+        if (idx[0] != kNoIdx && rk < K) {
+            sm.ccode[wave * K + rk] = code[0];
+            sm.cidx[wave * K + rk] = idx[0];
+            sm.clist[wave * K + rk] = tid;
+        }
+    }
+    if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
+    sync();
+    if (wave != 0) return;
+    if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
+    // B. rank the survivors (lane = slot); the K best heads' lists hold the pod's top K
+    int ntot = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) ntot += sm.wnv[w];
+    {
+        const bool in = lane < W * K;
+        const uint64_t sc = in ? sm.ccode[lane] : 0ull;
+        const int32_t si = in ? sm.cidx[lane] : kNoIdx;
+        const int32_t sl = in ? sm.clist[lane] : 0;
+        const int g = wave_rank(sc, si, sc, si);
+        if (si != kNoIdx && g < K) sm.keep[g] = sl;
+    }
+    wave_lds_order();
+    if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
+    // C. the kept lists' entries (lane holds entries lane + 64 p), ranked against each other
+    const int nkeep = ntot < K ? ntot : K;
+    uint64_t ec[EP];
+    int32_t ei[EP];
+    int nvalid = 0;
+#pragma unroll
+    for (int p = 0; p < EP; ++p) {
+        const int e = lane + 64 * p;
+        const bool in = e < E && e / KC < nkeep;
+        const int l = in ? sm.keep[e / KC] : 0;
+        ec[p] = in ? sm.code[l][e % KC] : 0ull;
+        ei[p] = in ? sm.idx[l][e % KC] : kNoIdx;
+        nvalid += __popcll(__ballot(ei[p] != kNoIdx));
+    }
+#pragma unroll
+    for (int p = 0; p < EP; ++p) {
+        int r = 0;
+#pragma unroll
+        for (int p2 = 0; p2 < EP; ++p2) r += wave_rank(ec[p2], ei[p2], ec[p], ei[p]);
+        if (ei[p] != kNoIdx && r < K) { sm.ocode[r] = ec[p]; sm.oidx[r] = ei[p]; }
+    }
+    wave_lds_order();
+    if (dbg) ts[5] = __builtin_amdgcn_s_memtime();
+    uint64_t gk = 0ull;
+    int32_t gi = kNoIdx;
+    bool gcut = false;
+    int64_t gcnt = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        if (sm.wci[w] != kNoIdx && (gi == kNoIdx || code_better(sm.wck[w], sm.wci[w], gk, gi))) { gk = sm.wck[w]; gi = sm.wci[w]; }
+        gcut = gcut || sm.wcut[w] != 0;
+        gcnt += sm.wcnt[w];
+    }
+    const int nout = nvalid < K ? nvalid : K;
+    // lists outside the kept K, or entries beyond K, remain: the output is cut
+    const bool left = ntot > nkeep || nvalid > K;
+    const int32_t cut_out = (gcut || left) ? 1 : 0;
+    if (lane < K) {
+        Rec r{};
+        const uint64_t mc = sm.ocode[lane < nout ? lane : 0];
+        const int32_t mi = sm.oidx[lane < nout ? lane : 0];
+        const bool ok = lane < nout && !(gi != kNoIdx && code_better(gk, gi, mc, mi));
+        if (ok) {
+            const NodeRec &nd = A.nodes[mi - A.node_offset];
+            const uint64_t u = (mc >> 63) ? (mc & 0x7fffffffffffffffull) : ~mc;  // inverse of key_code
+            r.key = __longlong_as_double((long long)u); r.idx = mi; r.valid = 1;
+            r.a[0] = load_i64<COH>(&nd.a[0]); r.a[1] = load_i64<COH>(&nd.a[1]); r.a[2] = load_i64<COH>(&nd.a[2]);
+            r.labels = nd.labels; r.price = nd.price;  // never written during a call
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        r.pad = lane == 0 ? cut_out : 0;
+        if (A.lds_msg) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(&r);
+#pragma unroll
+            for (int x = 0; x < kRecWords; ++x) A.lds_msg[lane * kRecWords + x] = w[x];
+        } else {
+            store_rec<COH>(A.out_rec + (size_t)b * K + lane, r);
+        }
+    }
+    if (lane == 0) {
+        if (A.lds_msg) {
+            A.lds_msg[K * kRecWords] = (uint32_t)(uint64_t)gcnt;
+            A.lds_msg[K * kRecWords + 1] = (uint32_t)((uint64_t)gcnt >> 32);
+        } else {
+            store_i64<COH>(A.out_fc + b, gcnt);
+        }
+    }
+    if (dbg && lane == 0) {
+        ts[6] = __builtin_amdgcn_s_memtime();
+        for (int k = 1; k < 7; ++k) atomicAdd((unsigned long long *)&A.dbg[k - 1], (unsigned long long)(ts[k] - ts[k - 1]));
+        atomicAdd((unsigned long long *)&A.dbg[7], 1ull);
+    }
+}
+
 }  // namespace ksched

@@ -42,6 +42,10 @@ constexpr int kSW = kPipeScoreWaves;  // score waves per workgroup
 constexpr int kMW = kPipeWaves - kSW;  // merge waves
 constexpr int kMT = kMW * 64;          // merging threads: one per score workgroup's list (G <= kMT)
 constexpr int kPU = 4;                 // rows per score step (independent key chains)
+#ifndef KSCHED_SCREEN_PU
+#define KSCHED_SCREEN_PU 4
+#endif
+constexpr int kSPU = KSCHED_SCREEN_PU;  // rows per step of the screened scan's passes
 
 // ---- barrier of ONE role's waves (LDS counter; s_barrier would wait for the other role too) ----------
 __device__ __forceinline__ void role_sync(unsigned *ctr, unsigned &target, unsigned nwaves) {
@@ -187,12 +191,17 @@ __device__ __forceinline__ void topk_merge_u32(uint32_t (&t)[KC], const uint32_t
 // LDS layout of a score workgroup: PipeCtl | rows [R] | fold lists | merge scratch | exchange messages
 template <int KC, int K>
 struct ScoreLayout {
-    static constexpr size_t fold_bytes = (size_t)(kSW / 2) * KC * 64 * 12 + 64 * 4;
+    static constexpr size_t fold_list_bytes = (size_t)(kSW / 2) * KC * 64 * 12 + 64 * 4;
+    // the screened scan's bound lists [kSW][KC][64] u32, queue counts [kSW] and row queue [kSW][ceil(R / kSW)] u16
+    __host__ __device__ static size_t fold_bytes(int R) {
+        const size_t scr = (size_t)kSW * KC * 64 * 4 + kSW * 4 + (size_t)kSW * ((R + kSW - 1) / kSW) * 2;
+        return scr > fold_list_bytes ? scr : fold_list_bytes;
+    }
     static constexpr size_t merge_bytes = (sizeof(MergeSmem<KC, K, kMT>) + 15) / 16 * 16;
     static constexpr size_t msg_bytes = ((size_t)(1 + kMaxXchgRanks) * msg_words(K) * 4 + 15) / 16 * 16;
     __host__ __device__ static size_t rows_off() { return kPipeCtlBytes; }
     __host__ __device__ static size_t fold_off(int R) { return kPipeCtlBytes + (size_t)R * sizeof(NodeRec); }
-    __host__ __device__ static size_t merge_off(int R) { return fold_off(R) + (fold_bytes + 15) / 16 * 16; }
+    __host__ __device__ static size_t merge_off(int R) { return fold_off(R) + (fold_bytes(R) + 15) / 16 * 16; }
     __host__ __device__ static size_t msg_off(int R) { return merge_off(R) + merge_bytes; }
     __host__ __device__ static size_t total(int R) { return msg_off(R) + msg_bytes; }
 };
@@ -295,7 +304,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 pc->s_p0 = p0v;
                 pc->s_done = donev;
                 pc->s_stop = errv != 0 ? 3 : stop;
-                pc->s_scr = kScreen && b >= scr_off_until;
+                pc->s_scr = kScreen && !P.no_screen && b >= scr_off_until;
                 pc->s_ex = 0;
             }
         }
@@ -334,62 +343,71 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
 #pragma unroll
         for (int q = 0; q < KC; ++q) { key[q] = -__builtin_inf(); idx[q] = kNoIdx; }
         int32_t cnt = 0;
-        auto insert = [&](double ck, int32_t ci) {
-            bool moved = false;  // nodes arrive in ascending index: strict '>' keeps ties in index order
-#pragma unroll
-            for (int q = 0; q < KC; ++q) {
-                const bool sw = moved || ck > key[q];
-                moved = sw;
-                const double tk = key[q];
-                const int32_t ti = idx[q];
-                key[q] = sw ? ck : tk; idx[q] = sw ? ci : ti;
-                ck = sw ? tk : ck; ci = sw ? ti : ci;
-            }
-        };
         const bool scr = kScreen && pc->s_scr;  // workgroup-uniform
         if (scr) {
             // Bounds travel shifted by +1 as f32 bit patterns: every one is then 0 ("none") or a positive
             // float, whose bits order as unsigned integers (max/min without NaN canonicalisation).
             const float qc = screen_req(rc), qm = screen_req(rm), qp = screen_req(rp);
-            auto screen = [&](const NodeRec &nd, bool *f, float *s, float *fm) {
-                *f = fits(rc, rm, rp, sel, nd.a[0], nd.a[1], nd.a[2], nd.labels, LAB);
-                *s = screen_score(qc, qm, qp, nd.ys[0], nd.ys[1], nd.ys[2], fm);
+            const int Rv = (int)((n - g + G - 1) / G);  // rows of this workgroup that hold a node
+            // kPU rows per step, every load issued before any use and no branch in the step (a row past
+            // Rv re-reads row r0 and is masked)
+            struct Pre {
+                int64_t a0, a1, a2;
+                uint64_t lab;
+                float y0, y1, y2;
             };
-            // ---- pass 1: every row -- the predicate count, and the KC largest lower bounds (screen - eps)
-            // of the pairs that surely carry an eligible key ----
+            auto pre = [&](int r0, Pre (&x)[kSPU]) {
+#pragma unroll
+                for (int u = 0; u < kSPU; ++u) {
+                    const int r = r0 + u * kSW;
+                    const NodeRec &nd = rows[r < Rv ? r : r0];
+                    x[u].a0 = nd.a[0]; x[u].a1 = nd.a[1]; x[u].a2 = nd.a[2];
+                    x[u].lab = LAB ? nd.labels : 0ull;
+                    x[u].y0 = nd.ys[0]; x[u].y1 = nd.ys[1]; x[u].y2 = nd.ys[2];
+                }
+            };
+            // the pair's screen value, whether it is a lower bound, and whether the pair has a key at all
+            auto screen = [&](const Pre &x, bool *f, bool *el, bool *lo_ok) {
+                const bool okc = x.a0 >= rc, okm = x.a1 >= rm, okp = x.a2 >= rp;
+                *f = okc & okm & okp & (!LAB || (x.lab & sel) == sel);
+                *el = DOM == kDomAll || *f;
+                return screen_pair(qc, qm, qp, x.y0, x.y1, x.y2, okc, okm, okp, lo_ok);
+            };
+            // ---- pass 1: every row -- the predicate count, and the KC largest lower bounds of this pod's
+            // eligible keys ----
             uint32_t t[KC];
 #pragma unroll
             for (int q = 0; q < KC; ++q) t[q] = 0u;
-            for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
-                uint32_t xs[kPU];
+            for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
+                Pre x[kSPU];
+                pre(r0, x);
+                uint32_t xs[kSPU];
 #pragma unroll
-                for (int u = 0; u < kPU; ++u) {
-                    const int r = r0 + u * kSW;
-                    xs[u] = 0u;
-                    if (r < R && g + (int64_t)r * G < n) {  // wave-uniform
-                        bool f;
-                        float sc, fm;
-                        screen(rows[r], &f, &sc, &fm);
-                        cnt += f;
-                        // a fraction near 1 may zero the balanced part; NaN (unscreenable) fails every test
-                        const bool lo_ok = active && f && fm < 0.999f && sc > 0.0f;
-                        xs[u] = lo_ok ? __float_as_uint(sc + (1.0f - kScreenEps)) : 0u;
-                    }
+                for (int u = 0; u < kSPU; ++u) {
+                    const bool valid = r0 + u * kSW < Rv;
+                    bool f, el, lo_ok;
+                    const float v = screen(x[u], &f, &el, &lo_ok);
+                    cnt += (valid && f) ? 1 : 0;
+                    xs[u] = (valid && active && el && lo_ok) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
                 }
 #pragma unroll
-                for (int u = 0; u < kPU; ++u) {
-                    uint32_t x = xs[u];
+                for (int u = 0; u < kSPU; ++u) {
+                    uint32_t xv = xs[u];
 #pragma unroll
                     for (int q = 0; q < KC; ++q) {
-                        const uint32_t hi = t[q] > x ? t[q] : x;
-                        x = t[q] > x ? x : t[q];
+                        const uint32_t hi = t[q] > xv ? t[q] : xv;
+                        xv = t[q] > xv ? xv : t[q];
                         t[q] = hi;
                     }
                 }
             }
+            if (g == 0 && tid == 0) trace_at(P, b, 11);
             // ---- the workgroup's bound: the KC-th largest lower bound over every wave's list (the fold
             // area is free until the scan ends) ----
             uint32_t *sl = reinterpret_cast<uint32_t *>(fold);  // [kSW][KC][64]
+            int32_t *qcnt = reinterpret_cast<int32_t *>(sl + kSW * KC * 64);  // [kSW]
+            uint16_t *qrow = reinterpret_cast<uint16_t *>(qcnt + kSW);         // [kSW][QW]
+            const int QW = (R + kSW - 1) / kSW;
 #pragma unroll
             for (int q = 0; q < KC; ++q) sl[(wave * KC + q) * 64 + lane] = t[q];
             sync();
@@ -401,40 +419,47 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 topk_merge_u32<KC>(t, u);
             }
             const float L = __uint_as_float(t[KC - 1]);  // + 1; 0 = fewer than KC bounds: everything passes
-            // ---- pass 2: a row is scored exactly (for every pod) when some pod's screen cannot prove its
-            // pair below L; a pair below L is below KC eligible keys of this workgroup, so it is in no
-            // top-KC list the exact scan would have produced ----
-            int nex = 0;
-            for (int r0 = wave; r0 < R; r0 += kSW * kPU) {
-                bool need[kPU], fs[kPU];
+            if (g == 0 && tid == 0) trace_at(P, b, 12);
+            // ---- pass 2: a row needs its exact scores when some pod's upper bound reaches L (a pair below
+            // L is below KC eligible keys of this workgroup, so it is in no top-KC list the exact scan would
+            // have produced); the wave queues such rows ----
+            int qn = 0;
+            for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
+                Pre x[kSPU];
+                pre(r0, x);
 #pragma unroll
-                for (int u = 0; u < kPU; ++u) {
-                    const int r = r0 + u * kSW;
-                    need[u] = false;
-                    fs[u] = false;
-                    if (r < R && g + (int64_t)r * G < n) {
-                        float sc, fm;
-                        screen(rows[r], &fs[u], &sc, &fm);
-                        const float hi = fs[u] ? sc + (1.0f + kScreenEps) : (DOM == kDomAll ? kScreenNoFitHi + 1.0f : 0.0f);
-                        need[u] = active && (DOM == kDomAll || fs[u]) && !(hi < L);
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kPU; ++u) {
-                    if (__ballot(need[u])) {  // wave-uniform; rows in ascending node order
-                        ++nex;
-                        const int r = r0 + u * kSW;
-                        const NodeRec &nd = rows[r];
-                        const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
-                        double k;
-                        const bool el = pair_key_fast<PRIO, DOM, F53>(fs[u], rc, rm, rp, rcf, rmf, rpf, ac, am, ap,
-                                                                      nd.af[0], nd.af[1], nd.af[2], nd.y[0], nd.y[1],
-                                                                      nd.y[2], y3, nd.price, &k);
-                        insert(el ? k : -__builtin_inf(), (int32_t)(P.node_offset + g + (int64_t)r * G));
-                    }
+                for (int u = 0; u < kSPU; ++u) {
+                    const bool valid = r0 + u * kSW < Rv;
+                    bool f, el, lo_ok;
+                    const float v = screen(x[u], &f, &el, &lo_ok);
+                    const bool need = valid && active && el && !(v + (1.0f + kScreenEps) < L);  // NaN: needed
+                    const bool any = __ballot(need) != 0;
+                    if (lane == 0) qrow[wave * QW + qn] = (uint16_t)(r0 + u * kSW);  // kept when any
+                    qn += any ? 1 : 0;
                 }
             }
-            if (nex && lane == 0) atomicAdd(&pc->s_ex, nex);
+            if (lane == 0) qcnt[wave] = qn;
+            if (g == 0 && tid == 0) trace_at(P, b, 14);
+            sync();
+            // ---- the queued rows, dealt round-robin to the waves (balanced), scored exactly for every pod;
+            // arrival order is not node order, so the insert ranks ties by node index ----
+            int base[kSW], tot = 0;
+#pragma unroll
+            for (int w = 0; w < kSW; ++w) { base[w] = tot; tot += qcnt[w]; }
+            for (int e = wave; e < tot; e += kSW) {
+                int w = 0;
+#pragma unroll
+                for (int v = 1; v < kSW; ++v) w += e >= base[v] ? 1 : 0;
+                const int r = qrow[w * QW + (e - base[w])];
+                const NodeRec &nd = rows[r];
+                const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+                const bool f = fits(rc, rm, rp, sel, ac, am, ap, nd.labels, LAB);
+                double k;
+                const bool el = pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, ac, am, ap, nd.af[0], nd.af[1],
+                                                              nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k);
+                if (el) list_insert_ordered<KC>(key, idx, k, (int32_t)(P.node_offset + g + (int64_t)r * G));
+            }
+            if (wave == 0 && lane == 0) pc->s_ex = tot;
         } else
         // kPU rows per step: their keys are independent f64 chains the scheduler interleaves; inserted
         // in ascending node order afterwards
@@ -507,6 +532,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (wave == 0) {
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
             if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
+            if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap) P.trace[b * kTraceCols + 13] = (uint64_t)pc->s_ex;
             // s_cnt: every wave added before the last fold barrier
             if (active) {
                 Cand *dst = part + ((size_t)lane * G + g) * KC;
@@ -620,7 +646,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *smem, con
         for (int m = g; m < P.B; m += G) {
             const bool xchg = P.R > 1 && p0 + m < NP;  // uniform over the merge waves
             ma.lds_msg = xchg ? s_msg : nullptr;
-            merge_pod_body<KC, K, true, kMT>(ma, m, mtid, ms, sync);
+            merge_pod_fast<KC, K, true, kMT>(ma, m, mtid, ms, sync);
             if (xchg) {
                 // this rank's list of pod m -> slot (a % 4, rank, m) of every rank's ring; then the R lists of
                 // pod m from this rank's ring -> rank merge -> the commit's list (lring)
