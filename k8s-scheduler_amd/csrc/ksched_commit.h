@@ -241,7 +241,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     if constexpr (!COH) load_lists();
 
     // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
     const int nin = COH ? L->xcount : A.xin->count;  // <= 64
@@ -311,7 +311,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     double my_score = 0.0;
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
     int nT = nin, done = nb, W = 64;
-    int64_t placed = 0, nrounds = 0, nfail = 0;
+    int64_t placed = 0, nrounds = 0, nfail = 0, niters = 0;
     if (wave == 0) {
         fcc = pj ? (int32_t)(fc0v + m.dfacc[lane]) : 0;
         cut = cut0;
@@ -333,31 +333,35 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         if (dbg) t_mark = __builtin_amdgcn_s_memtime();
         if (wave == 0) {
             const int cend = (c + W < nb) ? c + W : nb;
-            // Guesses by fixpoint iteration, lane = pod: g_i = the first list entry of pod i that is neither
-            // confirmed-taken nor proposed by a pod < i (own[pos] < i) in the previous iteration.  Pod i's
-            // proposal is final once those of all pods < i are, so the fixpoint is reached after at most
-            // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
-            // the rule (99 %), it is reached after two.
+            // Guesses in pod order (the sequential greedy): pod i takes its first list entry that is neither
+            // confirmed-taken nor guessed by an earlier pod of the round.  Lane = pod holds its entries' table
+            // positions and the mask of those not confirmed-taken; the pods' guesses so far sit in `chosen`
+            // (lane t: pod t's guessed table position), so "guessed earlier" is one ballot -- no LDS in the loop.
             const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
             const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
-            int32_t pq = -1, ph = kSpcInvalid;  // current proposal (list position, table position)
-            for (int it = 0;; ++it) {
-                int32_t nq = -1, nh = kSpcInvalid;
-                if (act) {
-                    for (int qq = 0; qq < K; ++qq) {
-                        const int pos = m.HP[qq * 64 + lane];
-                        if (pos == kSpcInvalid) break;  // valid entries form a prefix
-                        const bool tk = (m.tkc[pos >> 5] >> (pos & 31)) & 1u;
-                        if (!tk && m.own[pos] >= lane) { nq = qq; nh = pos; break; }
-                    }
+            int32_t hp[K];
+            uint32_t am = 0;
+#pragma unroll
+            for (int qq = 0; qq < K; ++qq) hp[qq] = m.HP[qq * 64 + lane];
+#pragma unroll
+            for (int qq = 0; qq < K; ++qq) {  // kSpcInvalid's table bit is always set: ends the list
+                const int pos = hp[qq];
+                am |= ((m.tkc[pos >> 5] >> (pos & 31)) & 1u) ? 0u : (1u << qq);
+            }
+            int32_t pq = -1, ph = kSpcInvalid;  // this pod's guess (list position, table position)
+            int32_t chosen = -1;
+            ++niters;
+            for (uint64_t actm = __ballot(act); actm; actm &= actm - 1) {
+                const int i = (int)__builtin_ctzll(actm);
+                const uint32_t ami = (uint32_t)__builtin_amdgcn_readlane((int)am, i);
+#pragma unroll
+                for (int qq = 0; qq < K; ++qq) {
+                    if (!((ami >> qq) & 1u)) continue;  // uniform
+                    const int32_t P = __builtin_amdgcn_readlane(hp[qq], i);
+                    if (__ballot(chosen == P)) continue;  // guessed by an earlier pod
+                    if (lane == i) { pq = qq; ph = P; chosen = P; }
+                    break;
                 }
-                const bool changed = __ballot(act && nq != pq) != 0;
-                if (act && pq >= 0) m.own[ph] = 64;
-                lds_order();
-                pq = nq; ph = nh;
-                if (!changed && it > 0) break;
-                if (act && pq >= 0) atomicMin(&m.own[ph], lane);
-                lds_order();
             }
             const uint64_t gm = __ballot(act && pq >= 0);
             if (lane >= c && lane < cend) {
@@ -647,7 +651,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             plan_after_commit<COH>(A, done < nb, p0 + done);
         }
         if (A.dbg) {
-            A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1;
+            A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1; A.dbg[5] += niters;
             A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
             A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
             A.dbg[6] += t_pre;

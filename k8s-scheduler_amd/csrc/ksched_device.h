@@ -255,6 +255,25 @@ __host__ __device__ __forceinline__ float screen_recip(int64_t a) {
 __host__ __device__ __forceinline__ float screen_req(int64_t r) {
     return (r >= 0 && r < (1ll << 52)) ? (float)r : __builtin_nanf("");
 }
+// A fraction q = RN(RN(r) * RN(1/a)) (f32) is within 3u = 1.8e-7 (relative) of r/a: below kFracLo it proves
+// r < a, above kFracHi r > a; in between (or NaN) the int64 compare decides.
+constexpr float kFracLo = 1.0f - 0x1p-20f;
+constexpr float kFracHi = 1.0f + 0x1p-20f;
+
+// The screen of one pair from its f32 fractions c, m, p; ok* = (a_k >= r_k) per resource, exact.
+__device__ __forceinline__ float screen_q(float c, float m, float p, bool okc, bool okm, bool okp, bool *lo_ok) {
+    const bool rf = okc & okm & okp;
+    const float fmax = __builtin_fmaxf(__builtin_fmaxf(c, m), p);
+    const float S = (c + m) + p;
+    const float Q = (c * c + m * m) + p * p;
+    const float poly = ((10.0f - (5.0f / 3.0f) * S) - (5.0f / 3.0f) * Q) + (5.0f / 9.0f) * (S * S);
+    const float nf = (5.0f / 3.0f) * (((okc ? 1.0f - c : 0.0f) + (okm ? 1.0f - m : 0.0f)) + (okp ? 1.0f - p : 0.0f)) +
+                     0.0f * S;
+    const float v = rf ? poly : nf;
+    *lo_ok = (rf ? fmax < 0.999f : true) && v > kScreenEps;  // false for NaN
+    return v;
+}
+
 // The screen of one pair.  ok* = (a_k >= r_k) per resource (exact int64 compares).  Returns the f32 value
 // (NaN: unscreenable, every comparison then asks for the exact score); *lo_ok: the pair surely carries an
 // eligible key >= value - eps (its value may serve as a lower bound: a polynomial pair with a fraction near 1

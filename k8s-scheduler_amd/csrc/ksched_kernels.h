@@ -358,6 +358,8 @@ struct PersistArgs {
     int32_t *err;           // device error word (5..9 = a persistent wait timed out)
     int64_t timeout_ticks;
     int32_t no_screen;      // diagnostics (KSCHED_NO_SCREEN): the exact scan in every batch
+    int32_t screen_ok;      // the screened scan's reciprocals fit in a score workgroup's LDS
+    int32_t screen_h;       // ... and so do pass 1's per-pair records
     // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
     uint64_t *trace;
     int64_t trace_cap;

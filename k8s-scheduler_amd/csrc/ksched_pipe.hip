@@ -22,6 +22,7 @@
 // every storing wave drained, one lane's counter update; sc1 loads after the poll) and every wait is
 // bounded (PersistArgs::timeout_ticks -> error words 5..11).  Snapshot semantics: score(b) sees every
 // commit up to b - 2, commit(b) inherits b - 1's (oracle/cpu_ref.c or_schedule_pipelined).
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -188,13 +189,51 @@ __device__ __forceinline__ void topk_merge_u32(uint32_t (&t)[KC], const uint32_t
     for (int q = 0; q < KC; ++q) t[q] = v[q];
 }
 
-// LDS layout of a score workgroup: PipeCtl | rows [R] | fold lists | merge scratch | exchange messages
+// One butterfly stage of the fold: this lane's sorted (key desc, idx asc) list and its DPP partner's (stage S
+// of wpartner: lane ^ 1, lane ^ 2, mirror within 8 lanes) -> the top KC of both, sorted, identical in both
+// lanes (bitonic: element-wise best of the list and the reversed partner list, then half-cleaners)
+template <int S, int KC>
+__device__ __forceinline__ void fold_stage(double (&k)[KC], int32_t (&ix)[KC]) {
+    double ok[KC];
+    int32_t oi[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+        ok[q] = wpartner_f64<S>(k[q]);
+        oi[q] = (int32_t)wpartner<S>((uint32_t)ix[q]);
+    }
+    double vk[KC];
+    int32_t vi[KC];
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+        const bool t = better(ok[KC - 1 - q], oi[KC - 1 - q], k[q], ix[q]);
+        vk[q] = t ? ok[KC - 1 - q] : k[q];
+        vi[q] = t ? oi[KC - 1 - q] : ix[q];
+    }
+#pragma unroll
+    for (int d = KC / 2; d >= 1; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < KC; ++i) {
+            if ((i & d) == 0) {
+                const bool t = better(vk[i + d], vi[i + d], vk[i], vi[i]);
+                const double a = vk[i], bb = vk[i + d];
+                const int32_t ai = vi[i], bi = vi[i + d];
+                vk[i] = t ? bb : a; vi[i] = t ? bi : ai;
+                vk[i + d] = t ? a : bb; vi[i + d] = t ? ai : bi;
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < KC; ++q) { k[q] = vk[q]; ix[q] = vi[q]; }
+}
+
+// LDS layout of a score workgroup: PipeCtl | rows [R] | screen reciprocals [R] | fold lists | merge scratch |
+// exchange messages | [screen records, when they fit]
 template <int KC, int K>
 struct ScoreLayout {
-    static constexpr size_t fold_list_bytes = (size_t)(kSW / 2) * KC * 64 * 12 + 64 * 4;
+    static constexpr size_t fold_list_bytes = (size_t)kSW * KC * 64 * 12 + 64 * 4;  // every wave's lists + s_cnt
     // the screened scan's bound lists [kSW][KC][64] u32, queue counts [kSW] and row queue [kSW][ceil(R / kSW)] u16
     __host__ __device__ static size_t fold_bytes(int R) {
-        const size_t scr = (size_t)kSW * KC * 64 * 4 + kSW * 4 + (size_t)kSW * ((R + kSW - 1) / kSW) * 2;
+        const size_t scr = (size_t)kSW * KC * 64 * 4 + kSW * 4 + (size_t)2 * kSW * ((R + kSW - 1) / kSW) * 2;
         return scr > fold_list_bytes ? scr : fold_list_bytes;
     }
     static constexpr size_t merge_bytes = (sizeof(MergeSmem<KC, K, kMT>) + 15) / 16 * 16;
@@ -204,6 +243,13 @@ struct ScoreLayout {
     __host__ __device__ static size_t merge_off(int R) { return fold_off(R) + (fold_bytes(R) + 15) / 16 * 16; }
     __host__ __device__ static size_t msg_off(int R) { return merge_off(R) + merge_bytes; }
     __host__ __device__ static size_t total(int R) { return msg_off(R) + msg_bytes; }
+    // the screened scan (when it fits): its f32 reciprocals, one 16-byte record per row ...
+    __host__ __device__ static size_t ysq_off(int R) { return total(R); }
+    __host__ __device__ static size_t total_screen(int R) { return total(R) + (size_t)R * 16; }
+    // ... and pass 1's per-pair records for pass 2: [kSW][ceil(R / kSW)][64] f16
+    __host__ __device__ static size_t hrec_off(int R) { return total_screen(R); }
+    __host__ __device__ static size_t hrec_bytes(int R) { return (size_t)kSW * ((R + kSW - 1) / kSW) * 64 * 2; }
+    __host__ __device__ static size_t total_with_hrec(int R) { return total_screen(R) + hrec_bytes(R); }
 };
 
 constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16; }
@@ -219,9 +265,9 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     const int R = P.rows_per_wg;
     NodeRec *rows = reinterpret_cast<NodeRec *>(smem + ScoreLayout<KC, K>::rows_off());
     char *fold = smem + ScoreLayout<KC, K>::fold_off(R);
-    double *s_key = reinterpret_cast<double *>(fold);                     // [W/2][KC][64]
-    int32_t *s_idx = reinterpret_cast<int32_t *>(fold + (size_t)(kSW / 2) * KC * 64 * 8);
-    int32_t *s_cnt = s_idx + (size_t)(kSW / 2) * KC * 64;                 // [64]
+    float4 *ysq = reinterpret_cast<float4 *>(smem + ScoreLayout<KC, K>::ysq_off(R));  // screen reciprocals, SoA rows
+    uint16_t *hrec = reinterpret_cast<uint16_t *>(smem + ScoreLayout<KC, K>::hrec_off(R));  // [kSW][QW][64] (P.screen_h)
+    int32_t *s_cnt = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 12);  // [64], after the fold lists
     constexpr int kST = kSW * 64;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -238,9 +284,11 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (j < n) reinterpret_cast<int4 *>(rows + r)[piece] = reinterpret_cast<const int4 *>(P.nodes + j)[piece];
     }
     sync();
-    for (int r = tid; r < R; r += kST) {  // the screen's f32 reciprocals (LDS rows only)
-        NodeRec &nd = rows[r];
-        nd.ys[0] = screen_recip(nd.a[0]); nd.ys[1] = screen_recip(nd.a[1]); nd.ys[2] = screen_recip(nd.a[2]);
+    if (P.screen_ok) {
+        for (int r = tid; r < R; r += kST) {  // the screen's f32 reciprocals, one 16-byte record per row
+            const NodeRec &nd = rows[r];
+            ysq[r] = make_float4(screen_recip(nd.a[0]), screen_recip(nd.a[1]), screen_recip(nd.a[2]), 0.0f);
+        }
     }
     // (batch 0's first barrier orders these writes before any export apply or scan)
     const double y3 = recip(3.0);
@@ -290,6 +338,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 const int64_t j = (int64_t)(int32_t)(uint32_t)x0 - P.node_offset;  // local row
                 if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
                 set_row(rows + j / G, (int64_t)x4, (int64_t)x5, (int64_t)x6);
+                if (P.screen_ok)
+                    ysq[j / G] = make_float4(screen_recip((int64_t)x4), screen_recip((int64_t)x5), screen_recip((int64_t)x6), 0.0f);
                 // the mergers read a candidate's state from its HBM row (sc1)
                 st_coh(&P.nodes[j].a[0], x4);
                 st_coh(&P.nodes[j].a[1], x5);
@@ -304,7 +354,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 pc->s_p0 = p0v;
                 pc->s_done = donev;
                 pc->s_stop = errv != 0 ? 3 : stop;
-                pc->s_scr = kScreen && !P.no_screen && b >= scr_off_until;
+                pc->s_scr = kScreen && P.screen_ok && !P.no_screen && b >= scr_off_until;
                 pc->s_ex = 0;
             }
         }
@@ -349,65 +399,128 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             // float, whose bits order as unsigned integers (max/min without NaN canonicalisation).
             const float qc = screen_req(rc), qm = screen_req(rm), qp = screen_req(rp);
             const int Rv = (int)((n - g + G - 1) / G);  // rows of this workgroup that hold a node
-            // kPU rows per step, every load issued before any use and no branch in the step (a row past
-            // Rv re-reads row r0 and is masked)
-            struct Pre {
-                int64_t a0, a1, a2;
-                uint64_t lab;
-                float y0, y1, y2;
-            };
-            auto pre = [&](int r0, Pre (&x)[kSPU]) {
-#pragma unroll
-                for (int u = 0; u < kSPU; ++u) {
-                    const int r = r0 + u * kSW;
-                    const NodeRec &nd = rows[r < Rv ? r : r0];
-                    x[u].a0 = nd.a[0]; x[u].a1 = nd.a[1]; x[u].a2 = nd.a[2];
-                    x[u].lab = LAB ? nd.labels : 0ull;
-                    x[u].y0 = nd.ys[0]; x[u].y1 = nd.ys[1]; x[u].y2 = nd.ys[2];
+            const int QW = (R + kSW - 1) / kSW;
+            const bool keep_h = P.screen_h != 0;      // pass 1 leaves a record per pair for pass 2
+            uint16_t *hw = hrec + (size_t)wave * QW * 64 + lane;
+            // One row for every pod of the batch: the f32 fractions decide the predicate unless one lies
+            // within 2^-20 of 1 or is NaN (then the int64 compares of the row decide, for every pod); the
+            // screen value, whether it bounds an eligible key from below, and whether the pair has a key.
+            auto row_screen = [&](int r, const float4 &y, bool valid, bool *f, bool *el, bool *lo_ok) {
+                const float c = qc * y.x, m = qm * y.y, p = qp * y.z;
+                bool okc = c < kFracLo, okm = m < kFracLo, okp = p < kFracLo;
+                const bool amb = !(okc || c > kFracHi) || !(okm || m > kFracHi) || !(okp || p > kFracHi);
+                uint64_t lab = 0;
+                if (__ballot(valid && amb)) {  // wave-uniform, rare
+                    const NodeRec &nd = rows[r];
+                    okc = nd.a[0] >= rc; okm = nd.a[1] >= rm; okp = nd.a[2] >= rp;
                 }
-            };
-            // the pair's screen value, whether it is a lower bound, and whether the pair has a key at all
-            auto screen = [&](const Pre &x, bool *f, bool *el, bool *lo_ok) {
-                const bool okc = x.a0 >= rc, okm = x.a1 >= rm, okp = x.a2 >= rp;
-                *f = okc & okm & okp & (!LAB || (x.lab & sel) == sel);
+                if (LAB) lab = rows[r].labels;
+                *f = okc & okm & okp & (!LAB || (lab & sel) == sel);
                 *el = DOM == kDomAll || *f;
-                return screen_pair(qc, qm, qp, x.y0, x.y1, x.y2, okc, okm, okp, lo_ok);
+                return screen_q(c, m, p, okc, okm, okp, lo_ok);
             };
-            // ---- pass 1: every row -- the predicate count, and the KC largest lower bounds of this pod's
-            // eligible keys ----
+            // ---- pass 1: every row -- the predicate count, the KC largest lower bounds of this pod's eligible
+            // keys, and (keep_h) the pair's upper bound as an f16 record for pass 2 ----
             uint32_t t[KC];
 #pragma unroll
             for (int q = 0; q < KC; ++q) t[q] = 0u;
-            for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
-                Pre x[kSPU];
-                pre(r0, x);
-                uint32_t xs[kSPU];
+            uint32_t *sl = reinterpret_cast<uint32_t *>(fold);  // [kSW][KC][64] (the fold area is free until
+            int32_t *qcnt = reinterpret_cast<int32_t *>(sl + kSW * KC * 64);  // [kSW]      the scan ends)
+            uint16_t *qrow = reinterpret_cast<uint16_t *>(qcnt + kSW);         // [kSW][QW] rows for the exact phase
+            uint16_t *arow = qrow + kSW * QW;                                  // [kSW][QW] rows with an ambiguous fraction
+            int na = 0;
+            if (keep_h) {
+                // branch-free: a pair whose fraction is ambiguous (within 2^-20 of 1, or NaN) contributes no
+                // bound, gets a NaN record (scored exactly if it can matter) and its predicate is counted
+                // exactly after the loop, from its row's int64 values
+                for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
+                    float4 yv[kSPU];
+                    uint64_t lb[kSPU];
 #pragma unroll
-                for (int u = 0; u < kSPU; ++u) {
-                    const bool valid = r0 + u * kSW < Rv;
-                    bool f, el, lo_ok;
-                    const float v = screen(x[u], &f, &el, &lo_ok);
-                    cnt += (valid && f) ? 1 : 0;
-                    xs[u] = (valid && active && el && lo_ok) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        yv[u] = ysq[r < Rv ? r : r0];
+                        lb[u] = LAB ? rows[r < Rv ? r : r0].labels : 0ull;
+                    }
+                    uint32_t xs[kSPU];
+#pragma unroll
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        const bool valid = r < Rv;
+                        const float c = qc * yv[u].x, m = qm * yv[u].y, p = qp * yv[u].z;
+                        const bool okc = c < kFracLo, okm = m < kFracLo, okp = p < kFracLo;
+                        const bool amb = !(okc || c > kFracHi) || !(okm || m > kFracHi) || !(okp || p > kFracHi);
+                        const bool f = okc & okm & okp & (!LAB || (lb[u] & sel) == sel);
+                        const bool el = DOM == kDomAll || f;
+                        bool lo_ok;
+                        const float v = screen_q(c, m, p, okc, okm, okp, &lo_ok);
+                        cnt += (valid && f && !amb) ? 1 : 0;
+                        xs[u] = (valid && active && el && lo_ok && !amb) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
+                        // 10 - h >= v: h = f16 of (10 - v), rounded down by a relative 2^-10 and 2^-24 absolute
+                        // (f16 rounding is within 2^-11 relative); +inf (never needed) without a key; NaN stays NaN
+                        const float w = 10.0f - v;
+                        const float wd = w - __builtin_fabsf(w) * 0x1p-10f - 0x1p-24f;
+                        if (valid)
+                            hw[(size_t)(r >> 3) * 64] =
+                                __half_as_ushort(__float2half_rn(amb ? __builtin_nanf("") : (el ? wd : __builtin_inff())));
+                        const bool anya = __ballot(valid && amb) != 0;
+                        if (lane == 0) arow[wave * QW + na] = (uint16_t)r;  // kept when anya
+                        na += anya ? 1 : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSPU; ++u) {
+                        uint32_t xv = xs[u];
+#pragma unroll
+                        for (int q = 0; q < KC; ++q) {
+                            const uint32_t hi = t[q] > xv ? t[q] : xv;
+                            xv = t[q] > xv ? xv : t[q];
+                            t[q] = hi;
+                        }
+                    }
                 }
+                // the ambiguous pairs' predicate, exactly
+                for (int e = 0; e < na; ++e) {
+                    const int r = arow[wave * QW + e];
+                    const NodeRec &nd = rows[r];
+                    const float4 y = ysq[r];
+                    const float c = qc * y.x, m = qm * y.y, p = qp * y.z;
+                    const bool amb = !(c < kFracLo || c > kFracHi) || !(m < kFracLo || m > kFracHi) ||
+                                     !(p < kFracLo || p > kFracHi);
+                    cnt += (amb && fits(rc, rm, rp, sel, nd.a[0], nd.a[1], nd.a[2], nd.labels, LAB)) ? 1 : 0;
+                }
+            } else {
+                for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
+                    float4 yv[kSPU];
 #pragma unroll
-                for (int u = 0; u < kSPU; ++u) {
-                    uint32_t xv = xs[u];
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        yv[u] = ysq[r < Rv ? r : r0];
+                    }
+                    uint32_t xs[kSPU];
 #pragma unroll
-                    for (int q = 0; q < KC; ++q) {
-                        const uint32_t hi = t[q] > xv ? t[q] : xv;
-                        xv = t[q] > xv ? xv : t[q];
-                        t[q] = hi;
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        const bool valid = r < Rv;
+                        bool f, el, lo_ok;
+                        const float v = row_screen(valid ? r : r0, yv[u], valid, &f, &el, &lo_ok);
+                        cnt += (valid && f) ? 1 : 0;
+                        xs[u] = (valid && active && el && lo_ok) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSPU; ++u) {
+                        uint32_t xv = xs[u];
+#pragma unroll
+                        for (int q = 0; q < KC; ++q) {
+                            const uint32_t hi = t[q] > xv ? t[q] : xv;
+                            xv = t[q] > xv ? xv : t[q];
+                            t[q] = hi;
+                        }
                     }
                 }
             }
             if (g == 0 && tid == 0) trace_at(P, b, 11);
             // ---- the workgroup's bound: the KC-th largest lower bound over every wave's list (the fold
             // area is free until the scan ends) ----
-            uint32_t *sl = reinterpret_cast<uint32_t *>(fold);  // [kSW][KC][64]
-            int32_t *qcnt = reinterpret_cast<int32_t *>(sl + kSW * KC * 64);  // [kSW]
-            uint16_t *qrow = reinterpret_cast<uint16_t *>(qcnt + kSW);         // [kSW][QW]
-            const int QW = (R + kSW - 1) / kSW;
 #pragma unroll
             for (int q = 0; q < KC; ++q) sl[(wave * KC + q) * 64 + lane] = t[q];
             sync();
@@ -424,18 +537,40 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             // L is below KC eligible keys of this workgroup, so it is in no top-KC list the exact scan would
             // have produced); the wave queues such rows ----
             int qn = 0;
-            for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
-                Pre x[kSPU];
-                pre(r0, x);
+            if (keep_h) {
+                const int nr = (Rv - wave + kSW - 1) / kSW;  // this wave's rows
+                for (int i0 = 0; i0 < nr; i0 += 8) {
+                    uint16_t hv[8];
 #pragma unroll
-                for (int u = 0; u < kSPU; ++u) {
-                    const bool valid = r0 + u * kSW < Rv;
-                    bool f, el, lo_ok;
-                    const float v = screen(x[u], &f, &el, &lo_ok);
-                    const bool need = valid && active && el && !(v + (1.0f + kScreenEps) < L);  // NaN: needed
-                    const bool any = __ballot(need) != 0;
-                    if (lane == 0) qrow[wave * QW + qn] = (uint16_t)(r0 + u * kSW);  // kept when any
-                    qn += any ? 1 : 0;
+                    for (int u = 0; u < 8; ++u) hv[u] = hw[(size_t)(i0 + u < nr ? i0 + u : i0) * 64];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const float vd = 10.0f - __half2float(__ushort_as_half(hv[u]));
+                        const bool need = i0 + u < nr && active && !(vd + (1.0f + kScreenEps) < L);  // NaN: needed
+                        const bool any = __ballot(need) != 0;
+                        if (lane == 0) qrow[wave * QW + qn] = (uint16_t)(wave + (i0 + u) * kSW);  // kept when any
+                        qn += any ? 1 : 0;
+                    }
+                }
+            } else {
+                for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
+                    float4 yv[kSPU];
+#pragma unroll
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        yv[u] = ysq[r < Rv ? r : r0];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kSPU; ++u) {
+                        const int r = r0 + u * kSW;
+                        const bool valid = r < Rv;
+                        bool f, el, lo_ok;
+                        const float v = row_screen(valid ? r : r0, yv[u], valid, &f, &el, &lo_ok);
+                        const bool need = valid && active && el && !(v + (1.0f + kScreenEps) < L);  // NaN: needed
+                        const bool any = __ballot(need) != 0;
+                        if (lane == 0) qrow[wave * QW + qn] = (uint16_t)r;  // kept when any
+                        qn += any ? 1 : 0;
+                    }
                 }
             }
             if (lane == 0) qcnt[wave] = qn;
@@ -500,51 +635,57 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         }
         if (g == 0 && tid == 0) trace_at(P, b, 8);
         const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
-        sync();  // s_cnt zeroed before any wave adds
+        sync();  // every wave's scan is done (the fold area is free); s_cnt was zeroed
         if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
-        // fold the wave lists pairwise: W -> W/2 -> ... -> 1 (a list that is cut when full folds into
-        // the top-KC of the union, again cut when full: DESIGN.md section 4)
+        // ---- fold: every wave's lists to LDS; then wave w merges pods 8w .. 8w+7 for all 8 source waves at
+        // once (lane = pod x source wave; three 8-lane butterfly merges of sorted lists) and stores them.  A
+        // list that is cut when full folds into the top-KC of the union, again cut when full.
+        double *fk = reinterpret_cast<double *>(fold);                                  // [kSW][KC][64]
+        int32_t *fi = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 8);    // [kSW][KC][64]
 #pragma unroll
-        for (int half = kSW / 2; half >= 1; half >>= 1) {
-            if (wave >= half && wave < 2 * half) {
-#pragma unroll
-                for (int q = 0; q < KC; ++q) {
-                    s_key[((wave - half) * KC + q) * 64 + lane] = key[q];
-                    s_idx[((wave - half) * KC + q) * 64 + lane] = idx[q];
-                }
-            }
-            sync();
-            if (wave < half) {
-#pragma unroll
-                for (int q = 0; q < KC; ++q) {
-                    const int32_t oi = s_idx[(wave * KC + q) * 64 + lane];
-                    if (oi == kNoIdx) break;
-                    list_insert_ordered<KC>(key, idx, s_key[(wave * KC + q) * 64 + lane], oi);
-                }
-            }
-            if (half > 1) sync();
+        for (int q = 0; q < KC; ++q) {
+            fk[(wave * KC + q) * 64 + lane] = key[q];
+            fi[(wave * KC + q) * 64 + lane] = idx[q];
         }
+        sync();
+        static_assert(kSW == 8, "the fold deals 8 pods to each of 8 waves");
+        const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch
+        const int src = lane & 7;               // ... and source wave
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            key[q] = fk[(src * KC + q) * 64 + pl];
+            idx[q] = fi[(src * KC + q) * 64 + pl];
+        }
+        fold_stage<0, KC>(key, idx);
+        fold_stage<1, KC>(key, idx);
+        fold_stage<2, KC>(key, idx);
         if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
         Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
         int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        if (pl < P.B && p0 + pl < NP) {  // every lane of the group holds the pod's list: lane src stores entry src
+            Cand *dst = part + ((size_t)pl * G + g) * KC;
+            if (src < KC) {
+                double kk = key[0];
+                int32_t ii = idx[0];
+#pragma unroll
+                for (int q = 1; q < KC; ++q) {
+                    kk = src == q ? key[q] : kk;
+                    ii = src == q ? idx[q] : ii;
+                }
+                st_coh(&dst[src].key, (uint64_t)__double_as_longlong(kk));
+                st_coh(&dst[src].idx, (uint64_t)(uint32_t)ii);  // idx + pad (0)
+            }
+            if (src == 7) st_coh(part_cnt + (size_t)pl * G + g, (uint64_t)(int64_t)s_cnt[pl]);
+        }
+        drain_stores();
+        sync();  // every wave's stores are drained
         if (wave == 0) {
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
             if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
             if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap) P.trace[b * kTraceCols + 13] = (uint64_t)pc->s_ex;
-            // s_cnt: every wave added before the last fold barrier
-            if (active) {
-                Cand *dst = part + ((size_t)lane * G + g) * KC;
-#pragma unroll
-                for (int q = 0; q < KC; ++q) {
-                    st_coh(&dst[q].key, (uint64_t)__double_as_longlong(key[q]));
-                    st_coh(&dst[q].idx, (uint64_t)(uint32_t)idx[q]);  // idx + pad (0)
-                }
-                st_coh(part_cnt + (size_t)lane * G + g, (uint64_t)(int64_t)s_cnt[lane]);
-            }
-            drain_stores();
-            // ---- arrive (the merge waves of workgroups 1 .. B wait for all G); wave 0 made every store ----
+            // ---- arrive (the merge waves of workgroups 1 .. B wait for all G) ----
             const int slot = (int)((nact - 1) % 4);
             if (lane == 0) {
                 if (g == 0) trace_at(P, b, 5);
@@ -803,9 +944,18 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PersistArgs P) {
 }
 
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
-hipError_t pipe_one(const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+hipError_t pipe_one(const PersistArgs &a0, int launch, PipeInfo *info, hipStream_t s) {
     auto fn = k_pipe<KC, K, PRIO, DOM, LAB, F53>;
-    const size_t sl = ScoreLayout<KC, K>::total(a.rows_per_wg), cl = commit_total_bytes<K>();
+    PersistArgs a = a0;
+    // the screened scan when its reciprocals fit beside everything else, keeping pass 1's per-pair records
+    // when those fit too
+    constexpr size_t kLds = (size_t)160 * 1024;
+    const int R = a.rows_per_wg;
+    a.screen_h = ScoreLayout<KC, K>::total_with_hrec(R) <= kLds ? 1 : 0;
+    a.screen_ok = ScoreLayout<KC, K>::total_screen(R) <= kLds ? 1 : 0;
+    const size_t sl = a.screen_h ? ScoreLayout<KC, K>::total_with_hrec(R)
+                                 : (a.screen_ok ? ScoreLayout<KC, K>::total_screen(R) : ScoreLayout<KC, K>::total(R));
+    const size_t cl = commit_total_bytes<K>();
     const size_t lds = sl > cl ? sl : cl;
     if (info) {
         hipFuncAttributes at{};

@@ -294,7 +294,7 @@ def test_persistent_pipeline_parity(gpu_available, oracle_mod, name, nn, pp):
     cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
     want = oracle_mod.schedule(cl, nthreads=8)
     for kw in (dict(topk=16, batch=64), dict(topk=8, batch=64, chunk_topk=8), dict(topk=4, batch=32, chunk_topk=4),
-               dict(topk=16, batch=16), dict(topk=16, batch=64, pipe_wgs=34)):
+               dict(topk=16, batch=16), dict(topk=16, batch=64, pipe_wgs=66)):
         got = run_engine(cl, MODE_BATCHED, **kw)
         assert_same(got, want, f"{name}/{kw}")
         assert got[4]["pipeline"] == "persistent", got[4]
