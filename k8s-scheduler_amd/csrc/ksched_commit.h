@@ -34,6 +34,7 @@ constexpr int kSpcHash = 1 << kSpcHashBits;
 constexpr int kSpcSlots = 128;    // previous batch's commits (<= 64) + this batch's (<= 64)
 constexpr int kSpcRow = kSpcSlots + 1;
 constexpr int kSpcInvalid = kSpcHash - 1;  // table position reserved for "no entry" (always taken)
+constexpr int kGS = 14;                     // words per guessed entry in SpcSmem::GS
 
 struct alignas(8) SpcSlot {
     int32_t idx;
@@ -66,7 +67,8 @@ struct SpcSmem {
     int64_t *pbx;     // [16 waves][64 pods] (slot << 32) | node of that best
     int32_t *ctl;     // [0] round start c, [1] window end, [2] stop
     int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none)
-    uint64_t *GS;     // [64 pods][5] node state words (a[3], labels, price) of each pod's guessed entry
+    uint64_t *GS;     // [64 pods][kGS] each pod's guessed entry: state a[3], labels, price, and the state after
+                      // the pod's commit n[3] with its (double) and refined reciprocals (computed once, lane = pod)
 };
 
 __device__ __forceinline__ uint32_t spc_hash(int32_t idx) {
@@ -204,7 +206,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
         m.own = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
-        m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * 5 * sizeof(uint64_t);
+        m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
         m.D = reinterpret_cast<int8_t *>(p);
     }
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
@@ -241,7 +243,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     if constexpr (!COH) load_lists();
 
     // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
     const int nin = COH ? L->xcount : A.xin->count;  // <= 64
@@ -333,10 +335,12 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         if (dbg) t_mark = __builtin_amdgcn_s_memtime();
         if (wave == 0) {
             const int cend = (c + W < nb) ? c + W : nb;
-            // Guesses in pod order (the sequential greedy): pod i takes its first list entry that is neither
-            // confirmed-taken nor guessed by an earlier pod of the round.  Lane = pod holds its entries' table
-            // positions and the mask of those not confirmed-taken; the pods' guesses so far sit in `chosen`
-            // (lane t: pod t's guessed table position), so "guessed earlier" is one ballot -- no LDS in the loop.
+            // Guesses by fixpoint iteration, lane = pod: g_i = the first list entry of pod i that is neither
+            // confirmed-taken nor proposed by a pod < i (own[pos] < i) in the previous iteration.  Pod i's
+            // proposal is final once those of all pods < i are, so the fixpoint is reached after at most
+            // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
+            // the rule (99 %), it is reached after two.  The entries' table positions and the mask of those
+            // not confirmed-taken are loaded once per round; an iteration probes own[] only.
             const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
             const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
             int32_t hp[K];
@@ -348,20 +352,27 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                 const int pos = hp[qq];
                 am |= ((m.tkc[pos >> 5] >> (pos & 31)) & 1u) ? 0u : (1u << qq);
             }
-            int32_t pq = -1, ph = kSpcInvalid;  // this pod's guess (list position, table position)
-            int32_t chosen = -1;
-            ++niters;
-            for (uint64_t actm = __ballot(act); actm; actm &= actm - 1) {
-                const int i = (int)__builtin_ctzll(actm);
-                const uint32_t ami = (uint32_t)__builtin_amdgcn_readlane((int)am, i);
+            if (!act) am = 0;
+            int32_t pq = -1, ph = kSpcInvalid;  // current proposal (list position, table position)
+            for (int it = 0;; ++it) {
+                ++niters;
+                int32_t nq = -1, nh = kSpcInvalid;
+                bool open = am != 0;  // still probing
 #pragma unroll
                 for (int qq = 0; qq < K; ++qq) {
-                    if (!((ami >> qq) & 1u)) continue;  // uniform
-                    const int32_t P = __builtin_amdgcn_readlane(hp[qq], i);
-                    if (__ballot(chosen == P)) continue;  // guessed by an earlier pod
-                    if (lane == i) { pq = qq; ph = P; chosen = P; }
-                    break;
+                    if (!__ballot(open)) break;  // uniform: every lane has its proposal
+                    if (open) {
+                        if (((am >> qq) & 1u) && m.own[hp[qq]] >= lane) { nq = qq; nh = hp[qq]; open = false; }
+                        else if ((am >> qq) <= 1u) open = false;  // no later candidate
+                    }
                 }
+                const bool changed = __ballot(act && nq != pq) != 0;
+                if (act && pq >= 0) m.own[ph] = 64;
+                lds_order();
+                pq = nq; ph = nh;
+                if (!changed && it > 0) break;
+                if (act && pq >= 0) atomicMin(&m.own[ph], lane);
+                lds_order();
             }
             const uint64_t gm = __ballot(act && pq >= 0);
             if (lane >= c && lane < cend) {
@@ -385,29 +396,46 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         {
             double pk = -__builtin_inf();
             int32_t pi = kNoIdx, ps = -1;
-            // the guessed entries' snapshot state, staged in LDS by every thread at once (one memory latency
-            // for the round; the evaluation below then holds no per-pod arrays in registers)
-            for (int e = tid; e < 64 * 5; e += kSpcThreads) {
-                const int k = e / 5, w = e % 5;
-                if (k >= rc0 && k < rce && m.gn[k] >= 0) {
-                    const uint64_t *src = reinterpret_cast<const uint64_t *>(A.lists + (size_t)k * K + m.gq[k]) + 2 + w;
-                    m.GS[e] = COH ? ld_coh(src) : *src;
-                }
+            // the guessed entries' snapshot state and the state after the guessing pod's commit, with its
+            // doubles and reciprocals, staged in LDS once per guess by the guessing pod's own lane (wave 0)
+            if (wave == 0 && lane >= rc0 && lane < rce && m.gn[lane] >= 0) {
+                const uint64_t *src = reinterpret_cast<const uint64_t *>(A.lists + (size_t)lane * K + m.gq[lane]) + 2;
+                uint64_t v[5];
+#pragma unroll
+                for (int w = 0; w < 5; ++w) v[w] = COH ? ld_coh(src + w) : src[w];
+                // commit of pod `lane`: used += request, ONE pod (anchor/predicate.go:99-102)
+                const int64_t n0 = wsub((int64_t)v[0], rc), n1 = wsub((int64_t)v[1], rm), n2 = wsub((int64_t)v[2], 1);
+                const double nf0 = (double)n0, nf1 = (double)n1, nf2 = (double)n2;
+                uint64_t *o = m.GS + (size_t)lane * kGS;
+#pragma unroll
+                for (int w = 0; w < 5; ++w) o[w] = v[w];
+                o[5] = (uint64_t)n0; o[6] = (uint64_t)n1; o[7] = (uint64_t)n2;
+                o[8] = (uint64_t)__double_as_longlong(nf0); o[9] = (uint64_t)__double_as_longlong(nf1);
+                o[10] = (uint64_t)__double_as_longlong(nf2);
+                o[11] = (uint64_t)__double_as_longlong(recip_or_zero(n0, nf0));
+                o[12] = (uint64_t)__double_as_longlong(recip_or_zero(n1, nf1));
+                o[13] = (uint64_t)__double_as_longlong(recip_or_zero(n2, nf2));
             }
             __syncthreads();
             for (int k = rc0 + wave; k < rce; k += kSpcWaves) {
                 const int32_t g = __builtin_amdgcn_readfirstlane(m.gn[k]);
                 if (g < 0) continue;  // wave-uniform
                 const int s = __builtin_amdgcn_readfirstlane(m.gs[k]);
-                const int64_t a0 = (int64_t)m.GS[k * 5], a1 = (int64_t)m.GS[k * 5 + 1], a2 = (int64_t)m.GS[k * 5 + 2];
-                const uint64_t lab = m.GS[k * 5 + 3];
-                const float pr = __uint_as_float((uint32_t)m.GS[k * 5 + 4]);
-                // commit of pod k: used += request, ONE pod (anchor/predicate.go:99-102)
-                const int64_t n0 = wsub(a0, rl64(rc, k)), n1 = wsub(a1, rl64(rm, k)), n2 = wsub(a2, 1);
+                const uint64_t *gsk = m.GS + (size_t)k * kGS;
+                const int64_t a0 = (int64_t)gsk[0], a1 = (int64_t)gsk[1], a2 = (int64_t)gsk[2];
+                const uint64_t lab = gsk[3];
+                const float pr = __uint_as_float((uint32_t)gsk[4]);
+                const int64_t n0 = (int64_t)gsk[5], n1 = (int64_t)gsk[6], n2 = (int64_t)gsk[7];
                 const bool fo = fits(rc, rm, rp, sel, a0, a1, a2, lab, LAB);
                 const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
                 const int d = (int)fn - (int)fo;
-                const double kv = lane_key<PRIO, DOM, LAB, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, y3, pr);
+                double kv;
+                const bool el = pair_key_fast<PRIO, DOM, F53>(
+                    fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, __longlong_as_double((long long)gsk[8]),
+                    __longlong_as_double((long long)gsk[9]), __longlong_as_double((long long)gsk[10]),
+                    __longlong_as_double((long long)gsk[11]), __longlong_as_double((long long)gsk[12]),
+                    __longlong_as_double((long long)gsk[13]), y3, pr, &kv);
+                kv = el ? kv : -__builtin_inf();
                 Srow[s] = kv;
                 m.D[k * 64 + lane] = (int8_t)d;
                 if (lane > k) {
@@ -665,7 +693,7 @@ template <int K, int NT = kSpcThreads>
 constexpr size_t spc_lds_bytes() {
     return (size_t)64 * kSpcRow * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 + kSpcSlots * sizeof(SpcSlot) +
            (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 + kSpcSlots * 4 + 5 * 64 * 4 + 16 + (size_t)kSpcHash * 4 +
-           64 * 5 * 8 + 64 * 64;
+           64 * kGS * 8 + 64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
 

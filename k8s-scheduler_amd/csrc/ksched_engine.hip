@@ -606,13 +606,16 @@ int enqueue_persistent(ksched_ctx *c) {
     const int wgs = c->o.pipe_wgs > 0 ? std::min(c->o.pipe_wgs >= kXcds ? c->o.pipe_wgs / kXcds * kXcds : c->o.pipe_wgs,
                                                  c->cus)
                                       : c->cus;
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1, (int64_t)kPipeMergeThreads,
+    // merger workgroups: kPipeMergeSlots pods each, one slot per pod of a batch
+    const int M = (B + kPipeMergeSlots - 1) / kPipeMergeSlots;
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1 - M, (int64_t)kPipeMergeThreads,
                                                                (n_geom + 95) / 96}));
-    if (wgs < 2) return 1;
+    if (wgs < 2 + M) return 1;
     const int R = (int)((n_geom + G - 1) / G);
     PersistArgs a{};
     a.rows_per_wg = R;
     a.G = G;
+    a.M = M;
     a.B = B;
     PipeInfo info{};
     const bool f53 = c->fast53, lab = c->o.use_labels != 0;

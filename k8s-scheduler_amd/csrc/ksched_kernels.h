@@ -348,6 +348,7 @@ struct PersistArgs {
     PodArgs pods;
     Ctl *ctl;
     int32_t B, G, rows_per_wg;
+    int32_t M;              // merger workgroups (after the G score workgroups): kPipeMergeSlots pod slots each
     Cand *part;             // [2][B][G][KC]
     int64_t *part_cnt;      // [2][B][G]
     char *lring;            // 4 x {Rec [B][K]; int64 fc[B]}
@@ -452,11 +453,12 @@ __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int co
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }
 // The persistent pipeline (ksched_pipe.hip): ONE kernel of 1 + G workgroups x kPipeThreads, workgroup 0
-// the commit, workgroup 1 + g score waves (0 .. kPipeScoreWaves-1) + merge waves (the rest).
+// the commit, workgroups 1 .. G score, workgroups G + 1 .. G + M merge (kPipeMergeSlots pods each).
 constexpr int kPipeThreads = 768;
 constexpr int kPipeWaves = kPipeThreads / 64;
-constexpr int kPipeScoreWaves = 8;
-constexpr int kPipeMergeThreads = (kPipeWaves - kPipeScoreWaves) * 64;  // one per score workgroup's list
+constexpr int kPipeScoreWaves = kPipeWaves;  // a score workgroup scores with all its waves
+constexpr int kPipeMergeThreads = 256;       // one pod merge: one thread per score workgroup's list
+constexpr int kPipeMergeSlots = kPipeThreads / kPipeMergeThreads;  // pods a merger workgroup merges at once
 struct PipeInfo {
     size_t lds;         // dynamic LDS per workgroup (max of the commit's and a score workgroup's layout)
     size_t static_lds;

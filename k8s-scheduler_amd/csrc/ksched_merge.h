@@ -263,12 +263,19 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// how many lanes of this wave hold a (code, idx) better than (mc, mi) -- (code, idx) pairs are distinct
+// how many lanes of this wave hold a (code, idx) better than (mc, mi) -- (code, idx) pairs are distinct.
+// The 64 values travel around the wave by DPP wave_ror:1 (63 rotations, all VALU: no SGPR round trips).
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x13C, 0xF, 0xF, false);
+}
 __device__ __forceinline__ int wave_rank(uint64_t code, int32_t idx, uint64_t mc, int32_t mi) {
-    int r = 0;
-#pragma unroll
-    for (int l = 0; l < 64; ++l)
-        r += code_better(readlane_u64(code, l), __builtin_amdgcn_readlane(idx, l), mc, mi) ? 1 : 0;
+    uint32_t lo = (uint32_t)code, hi = (uint32_t)(code >> 32), ix = (uint32_t)idx;
+    int r = code_better(code, idx, mc, mi) ? 1 : 0;
+#pragma unroll 9
+    for (int l = 1; l < 64; ++l) {
+        lo = wave_ror1(lo); hi = wave_ror1(hi); ix = wave_ror1(ix);
+        r += code_better(((uint64_t)hi << 32) | lo, (int32_t)ix, mc, mi) ? 1 : 0;
+    }
     return r;
 }
 

@@ -39,9 +39,10 @@ namespace ksched {
 
 namespace {
 
-constexpr int kSW = kPipeScoreWaves;  // score waves per workgroup
-constexpr int kMW = kPipeWaves - kSW;  // merge waves
-constexpr int kMT = kMW * 64;          // merging threads: one per score workgroup's list (G <= kMT)
+constexpr int kSW = kPipeScoreWaves;  // score waves per score workgroup
+constexpr int kMT = kPipeMergeThreads; // threads of one pod merge: one per score workgroup's list (G <= kMT)
+constexpr int kMW = kMT / 64;          // waves of one pod merge
+constexpr int kMS = kPipeMergeSlots;   // pod merges per merger workgroup
 constexpr int kPU = 4;                 // rows per score step (independent key chains)
 #ifndef KSCHED_SCREEN_PU
 #define KSCHED_SCREEN_PU 4
@@ -236,13 +237,9 @@ struct ScoreLayout {
         const size_t scr = (size_t)kSW * KC * 64 * 4 + kSW * 4 + (size_t)2 * kSW * ((R + kSW - 1) / kSW) * 2;
         return scr > fold_list_bytes ? scr : fold_list_bytes;
     }
-    static constexpr size_t merge_bytes = (sizeof(MergeSmem<KC, K, kMT>) + 15) / 16 * 16;
-    static constexpr size_t msg_bytes = ((size_t)(1 + kMaxXchgRanks) * msg_words(K) * 4 + 15) / 16 * 16;
     __host__ __device__ static size_t rows_off() { return kPipeCtlBytes; }
     __host__ __device__ static size_t fold_off(int R) { return kPipeCtlBytes + (size_t)R * sizeof(NodeRec); }
-    __host__ __device__ static size_t merge_off(int R) { return fold_off(R) + (fold_bytes(R) + 15) / 16 * 16; }
-    __host__ __device__ static size_t msg_off(int R) { return merge_off(R) + merge_bytes; }
-    __host__ __device__ static size_t total(int R) { return msg_off(R) + msg_bytes; }
+    __host__ __device__ static size_t total(int R) { return fold_off(R) + (fold_bytes(R) + 15) / 16 * 16; }
     // the screened scan (when it fits): its f32 reciprocals, one 16-byte record per row ...
     __host__ __device__ static size_t ysq_off(int R) { return total(R); }
     __host__ __device__ static size_t total_screen(int R) { return total(R) + (size_t)R * 16; }
@@ -251,6 +248,22 @@ struct ScoreLayout {
     __host__ __device__ static size_t hrec_bytes(int R) { return (size_t)kSW * ((R + kSW - 1) / kSW) * 64 * 2; }
     __host__ __device__ static size_t total_with_hrec(int R) { return total_screen(R) + hrec_bytes(R); }
 };
+
+// LDS of a merger workgroup: kMS slots of {control words | merge scratch | exchange messages}
+struct alignas(16) MergeCtl {
+    unsigned mbar;
+    int32_t m_stop;
+    int64_t m_p0, m_done;
+};
+template <int KC, int K>
+struct MergeLayout {
+    static constexpr size_t ctl_bytes = 64;
+    static constexpr size_t merge_bytes = (sizeof(MergeSmem<KC, K, kMT>) + 15) / 16 * 16;
+    static constexpr size_t msg_bytes = ((size_t)(1 + kMaxXchgRanks) * msg_words(K) * 4 + 15) / 16 * 16;
+    static constexpr size_t slot_bytes = ctl_bytes + merge_bytes + msg_bytes;
+    static constexpr size_t total = kMS * slot_bytes;
+};
+static_assert(sizeof(MergeCtl) <= 64, "MergeCtl");
 
 constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16; }
 template <int K>
@@ -275,8 +288,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     const int G = P.G;
     const int64_t n = P.n_local, NP = P.pods.p;
     Ctl *ctl = P.ctl;
-    unsigned bar = 0;
-    auto sync = [&]() { role_sync(&pc->sbar, bar, kSW); };
+    auto sync = [&]() { __syncthreads(); };  // a score workgroup has no other role: plain barriers
     // this workgroup's rows j = g + r * G, resident in LDS for the whole call
     for (int e = tid; e < R * 6; e += kST) {
         const int r = e / 6, piece = e % 6;
@@ -461,10 +473,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const float w = 10.0f - v;
                         const float wd = w - __builtin_fabsf(w) * 0x1p-10f - 0x1p-24f;
                         if (valid)
-                            hw[(size_t)(r >> 3) * 64] =
+                            hw[(size_t)(r / kSW) * 64] =
                                 __half_as_ushort(__float2half_rn(amb ? __builtin_nanf("") : (el ? wd : __builtin_inff())));
                         const bool anya = __ballot(valid && amb) != 0;
-                        if (lane == 0) arow[wave * QW + na] = (uint16_t)r;  // kept when anya
+                        if (lane == 0 && na < QW) arow[wave * QW + na] = (uint16_t)r;  // kept when anya
                         na += anya ? 1 : 0;
                     }
 #pragma unroll
@@ -525,7 +537,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             for (int q = 0; q < KC; ++q) sl[(wave * KC + q) * 64 + lane] = t[q];
             sync();
             for (int w = 1; w < kSW; ++w) {
-                const int ow = (wave + w) & (kSW - 1);
+                const int ow = (wave + w) % kSW;
                 uint32_t u[KC];
 #pragma unroll
                 for (int q = 0; q < KC; ++q) u[q] = sl[(ow * KC + q) * 64 + lane];
@@ -548,7 +560,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const float vd = 10.0f - __half2float(__ushort_as_half(hv[u]));
                         const bool need = i0 + u < nr && active && !(vd + (1.0f + kScreenEps) < L);  // NaN: needed
                         const bool any = __ballot(need) != 0;
-                        if (lane == 0) qrow[wave * QW + qn] = (uint16_t)(wave + (i0 + u) * kSW);  // kept when any
+                        // kept when any; an index past QW only on a row past the wave's last (never kept)
+                        if (lane == 0 && qn < QW) qrow[wave * QW + qn] = (uint16_t)(wave + (i0 + u) * kSW);
                         qn += any ? 1 : 0;
                     }
                 }
@@ -568,7 +581,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const float v = row_screen(valid ? r : r0, yv[u], valid, &f, &el, &lo_ok);
                         const bool need = valid && active && el && !(v + (1.0f + kScreenEps) < L);  // NaN: needed
                         const bool any = __ballot(need) != 0;
-                        if (lane == 0) qrow[wave * QW + qn] = (uint16_t)r;  // kept when any
+                        if (lane == 0 && qn < QW) qrow[wave * QW + qn] = (uint16_t)r;  // kept when any
                         qn += any ? 1 : 0;
                     }
                 }
@@ -649,22 +662,33 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             fi[(wave * KC + q) * 64 + lane] = idx[q];
         }
         sync();
-        static_assert(kSW == 8, "the fold deals 8 pods to each of 8 waves");
-        const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch
-        const int src = lane & 7;               // ... and source wave
+        static_assert(kSW >= 8 && kSW <= 16, "the fold deals 8 pods to each of the first 8 waves");
+        const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch (waves 0..7)
+        const int src = lane & 7;               // ... and source wave (plus src + 8 when that exists)
+        const bool folds = wave < 8;
+        if (folds) {
 #pragma unroll
-        for (int q = 0; q < KC; ++q) {
-            key[q] = fk[(src * KC + q) * 64 + pl];
-            idx[q] = fi[(src * KC + q) * 64 + pl];
+            for (int q = 0; q < KC; ++q) {
+                key[q] = fk[(src * KC + q) * 64 + pl];
+                idx[q] = fi[(src * KC + q) * 64 + pl];
+            }
+            if (src + 8 < kSW) {
+#pragma unroll
+                for (int q = 0; q < KC; ++q) {
+                    const int32_t oi = fi[((src + 8) * KC + q) * 64 + pl];
+                    if (oi == kNoIdx) break;
+                    list_insert_ordered<KC>(key, idx, fk[((src + 8) * KC + q) * 64 + pl], oi);
+                }
+            }
+            fold_stage<0, KC>(key, idx);
+            fold_stage<1, KC>(key, idx);
+            fold_stage<2, KC>(key, idx);
         }
-        fold_stage<0, KC>(key, idx);
-        fold_stage<1, KC>(key, idx);
-        fold_stage<2, KC>(key, idx);
         if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
         Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
         int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
-        if (pl < P.B && p0 + pl < NP) {  // every lane of the group holds the pod's list: lane src stores entry src
+        if (folds && pl < P.B && p0 + pl < NP) {  // every lane of the group holds the pod's list: lane src stores entry src
             Cand *dst = part + ((size_t)pl * G + g) * KC;
             if (src < KC) {
                 double kk = key[0];
@@ -709,16 +733,17 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
 }
 
 // ------------------------------------------------------------------------------------------------
-// MERGE role (waves kSW .. 15 of workgroup 1 + g, g < B): pods m = g, g + G, ... of every batch
+// MERGE role (slot id = kMS * merger workgroup + slot, id < B; kMT threads): pods m = id, id + kMS * M, ...
+// of every batch
 // ------------------------------------------------------------------------------------------------
 template <int KC, int K>
-__device__ __forceinline__ void merge_role(const PersistArgs &P, char *smem, const int g) {
-    PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
-    const int R = P.rows_per_wg;
-    MergeSmem<KC, K, kMT> &ms = *reinterpret_cast<MergeSmem<KC, K, kMT> *>(smem + ScoreLayout<KC, K>::merge_off(R));
-    uint32_t *s_msg = reinterpret_cast<uint32_t *>(smem + ScoreLayout<KC, K>::msg_off(R));  // this rank's list
-    uint32_t *s_all = s_msg + msg_words(K);                                                  // every rank's list
-    const int mtid = threadIdx.x - kSW * 64;
+__device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, const int g) {
+    using ML = MergeLayout<KC, K>;
+    MergeCtl *pc = reinterpret_cast<MergeCtl *>(sbase);
+    MergeSmem<KC, K, kMT> &ms = *reinterpret_cast<MergeSmem<KC, K, kMT> *>(sbase + ML::ctl_bytes);
+    uint32_t *s_msg = reinterpret_cast<uint32_t *>(sbase + ML::ctl_bytes + ML::merge_bytes);  // this rank's list
+    uint32_t *s_all = s_msg + msg_words(K);                                                     // every rank's list
+    const int mtid = threadIdx.x % kMT;
     const int G = P.G;
     const int slot_prog = G + g;
     const int64_t NP = P.pods.p;
@@ -784,7 +809,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *smem, con
         ma.dbg = P.mdbg;
         ma.out_rec = reinterpret_cast<Rec *>(lb);
         ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
-        for (int m = g; m < P.B; m += G) {
+        for (int m = g; m < P.B; m += kMS * P.M) {
             const bool xchg = P.R > 1 && p0 + m < NP;  // uniform over the merge waves
             ma.lds_msg = xchg ? s_msg : nullptr;
             merge_pod_fast<KC, K, true, kMT>(ma, m, mtid, ms, sync);
@@ -931,15 +956,23 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PersistArgs P) {
 #endif
         return;
     }
-    const int g = blockIdx.x - 1;
-    PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
-    if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
-    __syncthreads();  // the only workgroup-wide barrier: before the roles part
+    if ((int)blockIdx.x <= P.G) {
+        PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
+        if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
+        __syncthreads();
 #ifndef KSCHED_PROBE_NO_SCORE
-    if (threadIdx.x < kSW * 64) score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, g);
+        score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, (int)blockIdx.x - 1);
 #endif
+        return;
+    }
+    // a merger workgroup: kMS independent pod slots of kMT threads
+    const int slot = (int)threadIdx.x / kMT;
+    const int id = ((int)blockIdx.x - 1 - P.G) * kMS + slot;
+    char *sbase = smem + (size_t)slot * MergeLayout<KC, K>::slot_bytes;
+    if (threadIdx.x % kMT == 0) reinterpret_cast<MergeCtl *>(sbase)->mbar = 0;
+    __syncthreads();  // the only workgroup-wide barrier: before the slots part
 #ifndef KSCHED_PROBE_NO_MERGE
-    if (threadIdx.x >= kSW * 64 && g < P.B) merge_role<KC, K>(P, smem, g);
+    if (id < P.B) merge_role<KC, K>(P, sbase, id);
 #endif
 }
 
@@ -955,8 +988,8 @@ hipError_t pipe_one(const PersistArgs &a0, int launch, PipeInfo *info, hipStream
     a.screen_ok = ScoreLayout<KC, K>::total_screen(R) <= kLds ? 1 : 0;
     const size_t sl = a.screen_h ? ScoreLayout<KC, K>::total_with_hrec(R)
                                  : (a.screen_ok ? ScoreLayout<KC, K>::total_screen(R) : ScoreLayout<KC, K>::total(R));
-    const size_t cl = commit_total_bytes<K>();
-    const size_t lds = sl > cl ? sl : cl;
+    const size_t cl = commit_total_bytes<K>(), ml = MergeLayout<KC, K>::total;
+    const size_t lds = sl > cl ? (sl > ml ? sl : ml) : (cl > ml ? cl : ml);
     if (info) {
         hipFuncAttributes at{};
         hipError_t e = hipFuncGetAttributes(&at, (const void *)fn);
@@ -967,14 +1000,14 @@ hipError_t pipe_one(const PersistArgs &a0, int launch, PipeInfo *info, hipStream
         info->spill = at.localSizeBytes;
     }
     if (!launch) return hipSuccess;
-    if (a.G > kMT || a.B > 64) return hipErrorInvalidValue;
+    if (a.G > kMT || a.B > 64 || a.M * kMS < a.B) return hipErrorInvalidValue;
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     if (launch == 1) {
         void *args[] = {const_cast<PersistArgs *>(&a)};
-        return hipLaunchCooperativeKernel((const void *)fn, dim3(1 + a.G), dim3(kPipeThreads), args, (unsigned)lds, s);
+        return hipLaunchCooperativeKernel((const void *)fn, dim3(1 + a.G + a.M), dim3(kPipeThreads), args, (unsigned)lds, s);
     }
-    hipLaunchKernelGGL(fn, dim3(1 + a.G), dim3(kPipeThreads), lds, s, a);
+    hipLaunchKernelGGL(fn, dim3(1 + a.G + a.M), dim3(kPipeThreads), lds, s, a);
     return hipGetLastError();
 }
 
