@@ -45,9 +45,15 @@ def pmc_summary(kernel, config, batch, world):
         return None
     out = {"traffic": k["fabric_bytes_per_launch"], "traffic_source": os.path.relpath(path, ROOT),
            "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE)"}
-    for f in ("hbm_gbs", "valu_busy_frac", "fp64_issue_frac"):
+    for f in ("hbm_gbs", "valu_busy_frac", "fp64_issue_frac", "active_inst_valu_frac"):
         if f in k:
             out[f"pmc_{f}"] = k[f]
+    c = k.get("counters_per_launch", {})
+    for f in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+        if f in c:
+            out[f"_{f}"] = c[f]
+    if "f64_valu_insts_per_launch" in k:
+        out["_F64"] = k["f64_valu_insts_per_launch"]
     return out
 
 
@@ -254,23 +260,27 @@ def main():
                   "HIP events on the score stream, one batch in 8 of one untimed pass",
     }
     if pmc:
-        roof.update({k: v for k, v in pmc.items() if k != "traffic"})
+        roof.update({k: v for k, v in pmc.items() if k != "traffic" and not k.startswith("_")})
     if persistent and mode == MODE_BATCHED:
         # What actually binds: the 24 B/pair HBM figure above is SURVEY 8d's
-        # bookkeeping -- node rows live in LDS for the whole call, so the score scan moves ~no HBM bytes.
-        # The scan is FP64-VALU work (ISA of the c4 loop: 40 FP64 + 70 other VALU wave-instructions per row of
-        # 64 pairs; FP64 at 4 cycles, other VALU at 2 cycles per wave64 instruction on a 16-lane SIMD), and
-        # the call is bound by the lag-2 dependency chain score -> merge -> commit -> score(b+2).
-        cyc_per_pair = (40 * 4 + 70 * 2) / 64.0
-        simds, clk = 256 * 4, 2.4e9
-        roof["bound_note"] = "bookkeeping: SURVEY 8d's 24 B/pair node re-read; the rows are LDS-resident"
-        roof["limiter"] = {
-            "what": "lag-2 dependency chain (score -> merge -> commit -> next score); score scan FP64-VALU",
-            "scan_valu_cycles_per_pair": cyc_per_pair,
-            "valu_busy_frac_chip": value / max(world, 1) * cyc_per_pair / (simds * clk),
+        # bookkeeping -- node rows live in LDS for the whole call, so the score scan moves ~no HBM bytes
+        # (traffic, from the FETCH_SIZE/WRITE_SIZE passes, is the merge handoff and control words).  The
+        # VALU figures are the SQ passes' counts per launch over the launch's pairs (a wave64 instruction
+        # covers 64 pairs: lane = pod); the call is bound by the lagged dependency chain
+        # score -> merge -> commit -> score of a later batch.
+        lim = {
+            "what": "lagged dependency chain (score -> merge -> commit -> later score); VALU issue latency",
             "fp64_tflops_algorithmic": value / max(world, 1) * FLOPS_PER_PAIR / 1e12,
             "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
         }
+        if pmc and score_pairs_per_launch > 0:
+            for f, name in (("_SQ_INSTS_VALU", "valu"), ("_F64", "fp64_valu"), ("_SQ_INSTS_SALU", "salu"),
+                            ("_SQ_INSTS_LDS", "lds")):
+                if f in pmc:
+                    lim[f"{name}_lane_insts_per_pair"] = pmc[f] * 64 / score_pairs_per_launch
+            lim["source"] = pmc["traffic_source"]
+        roof["bound_note"] = "bookkeeping: SURVEY 8d's 24 B/pair node re-read; the rows are LDS-resident"
+        roof["limiter"] = lim
     out = {
         "metric": "pod-node evaluations/sec",
         "value": value,

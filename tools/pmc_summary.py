@@ -33,7 +33,7 @@ F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"
 
 
 def family(name):
-    base = name.split("(")[0].split("<")[0].split("::")[-1]
+    base = name.replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split("::")[-1]
     for k, v in FAMILIES.items():
         if base.startswith(k):
             return base, v
