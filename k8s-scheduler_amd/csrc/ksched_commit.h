@@ -31,30 +31,33 @@ namespace {
 
 constexpr int kSpcHashBits = 11;  // touched + guessed node set (stale guesses stay until re-tagged)
 constexpr int kSpcHash = 1 << kSpcHashBits;
-constexpr int kSpcSlots = 128;    // previous batch's commits (<= 64) + this batch's (<= 64)
-constexpr int kSpcRow = kSpcSlots + 1;
+// touched-node slots: the inherited commits of the previous batch (lag 2: the stream pipeline) or of the
+// two previous batches (lag 3: the persistent pipeline), <= 64 each, + this batch's (<= 64)
+template <bool LAG3>
+constexpr int spc_slots() { return LAG3 ? 192 : 128; }
 constexpr int kSpcInvalid = kSpcHash - 1;  // table position reserved for "no entry" (always taken)
 constexpr int kGS = 14;                     // words per guessed entry in SpcSmem::GS
 
 struct alignas(8) SpcSlot {
     int32_t idx;
     int32_t mine;     // committed by this batch (exported)
-    int64_t s0[3];    // state at this batch's score snapshot
     int64_t sb[3];    // state when this batch's commit started
     int64_t cur[3];   // current state
     uint64_t labels;
     float price;
     int32_t pad;
 };
-static_assert(sizeof(SpcSlot) == 96, "SpcSlot");
+static_assert(sizeof(SpcSlot) == 72, "SpcSlot");
 
 struct SpcSmem {
     int32_t *hk;      // open-addressed table: node index per position (-1 = empty)
+    int32_t *ps;      // prologue only (aliases S): slot of each inherited node's table position
+    int64_t *s0;      // prologue only (aliases D): [inherited slot][3] state at this batch's score snapshot
     int32_t *HP;      // [K][64] table position of list entry (q, pod); kSpcInvalid for no entry
     uint32_t *tkc;    // [64] words: bit = position taken by a CONFIRMED touch (T)
     int32_t *ti;      // node index per slot
     SpcSlot *T;
-    double *S;        // [64 pods][kSpcRow] key of (pod, slot), -inf = not eligible
+    double *S;        // [64 pods][slots + 1] key of (pod, slot), -inf = not eligible
     double *LK;       // [K][64] list keys (lane-contiguous)
     int32_t *LI;      // [K][64] list node indices
     int8_t *D;        // [64 guessing pods][64 pods] predicate delta of the guessed commit
@@ -66,7 +69,8 @@ struct SpcSmem {
     double *pbk;      // [16 waves][64 pods] partial best key over the wave's guessed columns
     int64_t *pbx;     // [16 waves][64 pods] (slot << 32) | node of that best
     int32_t *ctl;     // [0] round start c, [1] window end, [2] stop
-    int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none)
+    int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none);
+                      // step 1 only (aliases pbk/pbx, which steps 2-3 use)
     uint64_t *GS;     // [64 pods][kGS] each pod's guessed entry: state a[3], labels, price, and the state after
                       // the pod's commit n[3] with its (double) and refined reciprocals (computed once, lane = pod)
 };
@@ -77,12 +81,15 @@ __device__ __forceinline__ uint32_t spc_hash(int32_t idx) {
 
 // Node -> position in an open-addressed table of every node the batch can touch (list entries and
 // inherited slots).  The position is a compact node id: "taken" is one bit per position.
-__device__ __forceinline__ int spc_pos_insert(int32_t *hk, int32_t idx) {
+__device__ __forceinline__ int spc_pos_insert(int32_t *hk, int32_t idx, bool *existed = nullptr) {
     uint32_t h = spc_hash(idx);
     for (;;) {
         if (h != kSpcInvalid) {
             const int32_t prev = atomicCAS(&hk[h], -1, idx);
-            if (prev == -1 || prev == idx) return (int)h;
+            if (prev == -1 || prev == idx) {
+                if (existed) *existed = prev == idx;
+                return (int)h;
+            }
         }
         h = (h + 1) & (kSpcHash - 1);
     }
@@ -94,13 +101,14 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int src) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-// plan_after_commit for the persistent commit: the plans come from (and go to) its LDS copy too
+// plan_after_commit for the persistent commit (batch b plans batch b + kPipeLag): the plans come from
+// (and go to) its LDS copy too
 __device__ __forceinline__ void persist_plan(const CommitArgs &A, bool truncated, int64_t cursor) {
     PersistLocal *L = A.loc;
-    const int64_t n1 = L->plan[(A.batch + 1) % kPlanRing];
+    const int64_t n1 = L->plan[(A.batch + kPipeLag - 1) % kPlanRing];
     int64_t nx = truncated ? cursor : (n1 < 0 ? -1 : n1 + A.B);
     if (nx >= A.pods.p) nx = -1;
-    L->plan[(A.batch + 2) % kPlanRing] = nx;
+    L->plan[(A.batch + kPipeLag) % kPlanRing] = nx;
     st_coh(A.plan2, (uint64_t)nx);
 }
 
@@ -156,6 +164,9 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                                                  Wait wait = Wait{}) {
     constexpr int kSpcWaves = NT / 64;
     constexpr int kSpcThreads = NT;
+    constexpr bool LAG3 = COH;  // the persistent pipeline runs at lag kPipeLag = 3
+    static_assert(!COH || kPipeLag == 3, "commit_spc_batch: the persistent pipeline's inheritance is lag 3");
+    constexpr int kSpcRow = spc_slots<LAG3>() + 1;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -169,6 +180,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             if (lane == 0) {
                 if (COH) {
                     st_coh(&A.xout->count, 0ull);
+                    L->xcount2 = L->xcount;
                     L->xcount = 0;
                     if (p0 >= 0 && p0 < A.pods.p) st_coh(&A.ctl->stats[3], (uint64_t)++L->stats[3]);
                     persist_plan(A, false, cursor);
@@ -193,11 +205,11 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.pbk = reinterpret_cast<double *>(p); p += (size_t)kSpcWaves * 64 * sizeof(double);
         m.pbx = reinterpret_cast<int64_t *>(p); p += (size_t)kSpcWaves * 64 * sizeof(int64_t);
         m.LK = reinterpret_cast<double *>(p); p += (size_t)K * 64 * sizeof(double);
-        m.T = reinterpret_cast<SpcSlot *>(p); p += (size_t)kSpcSlots * sizeof(SpcSlot);
+        m.T = reinterpret_cast<SpcSlot *>(p); p += (size_t)spc_slots<LAG3>() * sizeof(SpcSlot);
         m.hk = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
         m.HP = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
         m.tkc = reinterpret_cast<uint32_t *>(p); p += 64 * sizeof(uint32_t);
-        m.ti = reinterpret_cast<int32_t *>(p); p += kSpcSlots * sizeof(int32_t);
+        m.ti = reinterpret_cast<int32_t *>(p); p += spc_slots<LAG3>() * sizeof(int32_t);
         m.LI = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
         m.fcg = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.dfacc = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
@@ -205,9 +217,11 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.gq = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
-        m.own = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
         m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
         m.D = reinterpret_cast<int8_t *>(p);
+        m.ps = reinterpret_cast<int32_t *>(m.S);
+        m.own = reinterpret_cast<int32_t *>(m.pbk);
+        m.s0 = reinterpret_cast<int64_t *>(m.D);
     }
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
     // every wave: lane = pod j of the batch (lanes >= nb carry a zero request and are never read).
@@ -243,21 +257,61 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     if constexpr (!COH) load_lists();
 
     // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) { m.hk[w] = -1; m.own[w] = 64; }
+    // The inherited exports are loaded first, so their latency overlaps the table initialisation: wave 0
+    // lane e = entry e of the previous batch's export, wave 1 (lag 3) lane e = entry e of the one before it.
+    const int n1 = COH ? L->xcount : A.xin->count;  // <= 64 each
+    const int n2 = LAG3 ? L->xcount2 : 0;
+    XRec xi{};
+    if (wave == 0 && lane < n1) xi = load_xrec<COH>(&A.xin->e[lane]);
+    if (LAG3 && wave == 1 && lane < n2) xi = load_xrec<COH>(&A.xin2->e[lane]);
+    for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
-    const int nin = COH ? L->xcount : A.xin->count;  // <= 64
-    for (int e = tid; e < nin; e += kSpcThreads) {
-        const XRec xi = COH ? L->xe[e] : A.xin->e[e];
-        SpcSlot &x = m.T[e];
+    // slots [0, n1): the previous batch's commits; s0 = its start state (= this batch's snapshot at lag 2,
+    // and at lag 3 unless the node is also in the older export, which then overrides it below)
+    if (wave == 0 && lane < n1) {
+        SpcSlot &x = m.T[lane];
         x.idx = xi.idx; x.mine = 0;
-        for (int r = 0; r < 3; ++r) { x.s0[r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+        for (int r = 0; r < 3; ++r) { m.s0[lane * 3 + r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
         x.labels = xi.labels; x.price = xi.price; x.pad = 0;
-        m.ti[e] = xi.idx;
+        m.ti[lane] = xi.idx;
         const int h = spc_pos_insert(m.hk, xi.idx);
+        if (LAG3) m.ps[h] = lane;
         atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
     }
-    __syncthreads();
+    int nin = n1;
+    if constexpr (LAG3) {
+        // slots [n1, nin): nodes only the batch before the previous one committed; a node both committed
+        // keeps the previous batch's slot with the older start state as its snapshot state
+        __syncthreads();
+        if (wave == 1) {
+            bool fresh = false;
+            int h = 0;
+            if (lane < n2) {
+                bool existed;
+                h = spc_pos_insert(m.hk, xi.idx, &existed);
+                fresh = !existed;
+            }
+            const uint64_t fm = __ballot(fresh);
+            if (lane < n2) {
+                const int e = fresh ? n1 + __popcll(fm & ((1ull << lane) - 1ull)) : m.ps[h];
+                for (int r = 0; r < 3; ++r) m.s0[e * 3 + r] = xi.sb[r];
+                if (fresh) {
+                    SpcSlot &x = m.T[e];
+                    x.idx = xi.idx; x.mine = 0;
+                    for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+                    x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+                    m.ti[e] = xi.idx;
+                    atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
+                }
+            }
+            if (lane == 0) m.ctl[3] = n1 + __popcll(fm);
+        }
+        __syncthreads();
+        nin = m.ctl[3];
+    } else {
+        __syncthreads();
+    }
 
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
@@ -270,7 +324,8 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         int32_t pi = kNoIdx, ps = -1;
         for (int t = wave; t < nin; t += kSpcWaves) {
             const SpcSlot &x = m.T[t];
-            const bool f0 = fits(rc, rm, rp, sel, x.s0[0], x.s0[1], x.s0[2], x.labels, LAB);
+            const int64_t *x0 = m.s0 + t * 3;
+            const bool f0 = fits(rc, rm, rp, sel, x0[0], x0[1], x0[2], x.labels, LAB);
             const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
             dfl += (int)f1 - (int)f0;
             const double k = lane_key<PRIO, DOM, LAB, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
@@ -341,6 +396,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
             // the rule (99 %), it is reached after two.  The entries' table positions and the mask of those
             // not confirmed-taken are loaded once per round; an iteration probes own[] only.
+            for (int w = lane * 4; w < kSpcHash; w += 256) *reinterpret_cast<int4 *>(m.own + w) = make_int4(64, 64, 64, 64);
             const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
             const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
             int32_t hp[K];
@@ -446,7 +502,6 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                 if (lane == 0) {
                     SpcSlot &x = m.T[s];
                     x.idx = g; x.mine = 1;
-                    x.s0[0] = a0; x.s0[1] = a1; x.s0[2] = a2;
                     x.sb[0] = a0; x.sb[1] = a1; x.sb[2] = a2;  // untouched before this batch
                     x.cur[0] = n0; x.cur[1] = n1; x.cur[2] = n2;
                     x.labels = lab; x.price = pr; x.pad = 0;
@@ -592,7 +647,6 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                             SpcSlot &x = m.T[s];
                             if (kf == 1) {
                                 x.idx = wi;
-                                x.s0[0] = b0; x.s0[1] = b1; x.s0[2] = b2;
                                 x.sb[0] = b0; x.sb[1] = b1; x.sb[2] = b2;
                                 x.labels = lab; x.price = pr; x.pad = 0;
                                 m.ti[s] = wi;
@@ -655,13 +709,13 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             o.labels = x.labels; o.price = x.price; o.pad2 = 0;
             const int slot = base + __popcll(mask & ((1ull << lane) - 1));
             store_xrec<COH>(&A.xout->e[slot], o);
-            if (COH) L->xe[slot] = o;  // the next batch inherits it from LDS (every inherited read is done)
         }
         base += __popcll(mask);
     }
     if (lane == 0) {
         if (COH) {
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base);
+            L->xcount2 = L->xcount;
             L->xcount = base;
             L->cursor = p0 + done;
             st_coh(&A.ctl->cursor, (uint64_t)(p0 + done));
@@ -689,12 +743,16 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     return true;
 }
 
-template <int K, int NT = kSpcThreads>
+template <int K, int NT = kSpcThreads, bool LAG3 = false>
 constexpr size_t spc_lds_bytes() {
-    return (size_t)64 * kSpcRow * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 + kSpcSlots * sizeof(SpcSlot) +
-           (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 + kSpcSlots * 4 + 5 * 64 * 4 + 16 + (size_t)kSpcHash * 4 +
-           64 * kGS * 8 + 64 * 64;
+    return (size_t)64 * (spc_slots<LAG3>() + 1) * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 +
+           spc_slots<LAG3>() * sizeof(SpcSlot) + (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 +
+           spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
+// the prologue's aliases: the node -> slot map in S, the inherited snapshot states in D
+static_assert((size_t)64 * 129 * 8 >= kSpcHash * 4 && 64 * 64 >= 128 * 3 * 8, "SpcSmem prologue aliases");
+static_assert((size_t)(kSpcThreads / 64) * 64 * 16 >= kSpcHash * 4 && (kPipeThreads / 64) * 64 * 16 >= kSpcHash * 4,
+              "SpcSmem::own aliases pbk/pbx");
 
 }  // namespace ksched

@@ -365,7 +365,7 @@ int enqueue_batched(ksched_ctx *c) {
         return reinterpret_cast<XBuf *>(static_cast<char *>(c->d_xring) + (size_t)slot * xb);
     };
     Ctl *ctl = reinterpret_cast<Ctl *>(c->d_cursor);
-    HIPCHK(c, launch_ctl_init(ctl, pl.B, c->p, sS));
+    HIPCHK(c, launch_ctl_init(ctl, pl.B, c->p, 2, sS));
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
     if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
@@ -518,18 +518,19 @@ void print_persist_trace(ksched_ctx *c) {
     double scr[5] = {};  // WG 0 wave 0, screened batches: pass 1, bound merge, pass 2, exact phase (sums), exact rows
     int64_t nscr = 0;
     int64_t cnt = 0, first = -1, last = -1;
-    for (int64_t b = 2; b < c->trace_cap; ++b) {
-        if (!at(b, 0) || !at(b, 1) || !at(b, 2) || !at(b, 3) || !at(b, 4) || !at(b - 2, 4)) continue;
+    constexpr int64_t L = kPipeLag;
+    for (int64_t b = L; b < c->trace_cap; ++b) {
+        if (!at(b, 0) || !at(b, 1) || !at(b, 2) || !at(b, 3) || !at(b, 4) || !at(b - L, 4)) continue;
         if (first < 0) first = b;
         last = b;
         ++cnt;
-        sum[0] += (double)(int64_t)(at(b, 0) - at(b - 2, 4));  // commit(b-2) end -> score(b) start
+        sum[0] += (double)(int64_t)(at(b, 0) - at(b - L, 4));  // commit(b-L) end -> score(b) start
         sum[1] += (double)(int64_t)(at(b, 1) - at(b, 0));      // score (WG 0 start -> last arrival)
         sum[2] += (double)(int64_t)(at(b, 2) - at(b, 1));      // merge
         sum[3] += (double)(int64_t)(at(b, 3) - at(b, 2));      // last merge -> commit start
         sum[4] += (double)(int64_t)(at(b, 4) - at(b, 3));      // commit
         sum[5] += (double)(int64_t)(at(b, 3) - at(b - 1, 4));  // commit(b-1) end -> commit(b) start
-        sum[6] += (double)(int64_t)(at(b, 6) - at(b - 2, 4));  // WG 0: commit(b-2) end -> its poll returns
+        sum[6] += (double)(int64_t)(at(b, 6) - at(b - L, 4));  // WG 0: commit(b-L) end -> its poll returns
         sum[7] += (double)(int64_t)(at(b, 0) - at(b, 6));      // WG 0: plan loads + XBuf apply
         sum[8] += (double)(int64_t)(at(b, 5) - at(b, 0));      // WG 0: score + fold + list stores
         sum[9] += (double)(int64_t)(at(b, 7) - at(b, 1));      // last arrival -> merger past its poll
@@ -626,9 +627,10 @@ int enqueue_persistent(ksched_ctx *c) {
         fprintf(stderr, "[ksched pipe] G=%d rows/wg=%d LDS %zu+%zu B, %d VGPRs, %zu B scratch\n", G, R, info.lds,
                 info.static_lds, info.vgprs, info.spill);
     if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
-    // workspace: part lists [2][B][G][KC] + counts [2][B][G], list ring 4 x (B*K Rec + B fc), XBuf ring
-    const size_t part_b = align_up((size_t)2 * B * G * KC * sizeof(Cand), 256);
-    const size_t cnt_b = align_up((size_t)2 * B * G * sizeof(int64_t), 256);
+    // workspace: part lists [kPipeLag][B][G][KC] + counts [kPipeLag][B][G] (score(b + kPipeLag) reuses
+    // batch b's), list ring 4 x (B*K Rec + B fc), XBuf ring
+    const size_t part_b = align_up((size_t)kPipeLag * B * G * KC * sizeof(Cand), 256);
+    const size_t cnt_b = align_up((size_t)kPipeLag * B * G * sizeof(int64_t), 256);
     const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
     const size_t xb = align_up(xbuf_bytes(B), 256);
     const size_t prog_b = align_up((size_t)(G + B + 1) * kProgWords * 8, 256);
@@ -687,7 +689,7 @@ int enqueue_persistent(ksched_ctx *c) {
         a.mdbg = c->d_mdbg;
     }
     hipStream_t sS = c->stream;
-    HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, sS));
+    HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
     HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + 1) * kProgWords * 8, sS));
     // timing: the kernel (family 0) is bracketed by events on its stream -- one launch per call, so the

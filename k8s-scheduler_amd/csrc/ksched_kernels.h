@@ -87,6 +87,10 @@ struct alignas(8) XBuf {
 // Device-side pipeline control (one per context).  plan[] holds each in-flight batch's first pod
 // (ring of kPlanRing; -1 = nothing to do).  cursor/resync are written by k_commit, spec_next by k_plan.
 constexpr int kPlanRing = 8;
+// The persistent pipeline's lag: batch b is scored against the node state after commit(b - kPipeLag),
+// and commit(b) inherits the nodes the kPipeLag - 1 batches before it committed.
+// The stream pipeline runs at lag 2.
+constexpr int kPipeLag = 3;
 constexpr int kCtlReplicas = 8;
 struct alignas(128) CtlLine {
     unsigned long long v;
@@ -192,10 +196,8 @@ struct PersistLocal {
     int64_t plan[kPlanRing];
     int64_t cursor;
     int64_t stats[5];
-    int32_t xcount;   // the previous batch's export (this batch's inherited nodes)
-    int32_t pad;
-    XRec xe[64];
-    // the batch's pods, loaded before the wait for the merges (lane = pod)
+    int32_t xcount;   // entries of the previous batch's export
+    int32_t xcount2;  // entries of the export of the batch before it (both are inherited: lag kPipeLag)
 };
 
 struct CommitArgs {
@@ -208,6 +210,7 @@ struct CommitArgs {
     Ctl *ctl;
     int32_t B;
     const XBuf *xin;        // nodes committed by the previous batch (relative to this batch's snapshot)
+    const XBuf *xin2;       // persistent pipeline (lag 3): nodes committed two batches earlier; else null
     XBuf *xout;             // nodes committed by this batch
     OutArgs out;
     int64_t *dbg;           // diagnostics only (KSCHED_COMMIT_STAMPS): per-phase cycle sums, else null
@@ -335,7 +338,7 @@ hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t r
                           bool use_labels, uint8_t *reason, unsigned long long *counts, hipStream_t s);
 hipError_t launch_apply_delta(NodeRec *nodes, int64_t n, int64_t k, const int32_t *idx, const int64_t *d,
                               hipStream_t s);
-hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s);
+hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, int lag, hipStream_t s);
 
 // ---- persistent single-rank pipeline (ksched_persist.hip) -------------------------------------
 // One score grid of G workgroups (one per CU, the WG's node rows resident in LDS for the whole call)

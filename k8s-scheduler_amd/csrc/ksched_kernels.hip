@@ -837,7 +837,7 @@ __global__ __launch_bounds__(64) void k_commit(CommitArgs A) {
 
 // Pipeline control at the start of a batched call: batch 0 starts at pod 0, batch 1 speculatively at B;
 // every later plan is written by the commit two batches earlier (plan_after_commit).
-__global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
+__global__ void k_ctl_init(Ctl *ctl, int B, int64_t P, int lag) {
     if (threadIdx.x != 0) return;
     ctl->cursor = 0; ctl->spec_next = 0; ctl->resync = 0;
     for (int i = 0; i < 5; ++i) ctl->stats[i] = 0;
@@ -849,8 +849,8 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P) {
     for (int i = 0; i < kPlanRing; ++i) ctl->cursor_at[i] = 0;
     ctl->nact = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->plan[i] = -1;
-    ctl->plan[0] = P > 0 ? 0 : -1;
-    ctl->plan[1] = B < P ? B : -1;
+    // the first `lag` plans (batch b's commit plans batch b + lag)
+    for (int i = 0; i < lag; ++i) ctl->plan[i] = (int64_t)i * B < P ? (int64_t)i * B : -1;
 }
 
 // Write one batch's committed nodes into this rank's node rows.
@@ -1129,8 +1129,8 @@ hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t r
     return hipGetLastError();
 }
 
-hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, hipStream_t s) {
-    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, s, ctl, B, P);
+hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, int lag, hipStream_t s) {
+    hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, s, ctl, B, P, lag);
     return hipGetLastError();
 }
 

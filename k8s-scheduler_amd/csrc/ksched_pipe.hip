@@ -1,27 +1,27 @@
 // ksched_pipe.hip -- the batched pipeline as ONE persistent kernel.
 //
-// k_pipe, 1 + G workgroups of 1024 threads, one per CU (its LDS request excludes a second one), every
+// k_pipe, 1 + G + M workgroups of 768 threads, one per CU (its LDS request excludes a second one), every
 // workgroup resident for the whole call -- guaranteed by the launch itself: a cooperative launch of a
 // grid that the occupancy query admits (nothing of the call runs beside it), so no protocol below
-// assumes a dispatch order, a co-location or a second kernel.  Roles come from blockIdx / wave:
+// assumes a dispatch order, a co-location or a second kernel.  Roles come from blockIdx:
 //
-//   workgroup 0          the COMMIT (all 16 waves): per active batch, wait for its B merges, replay the
+//   workgroup 0          the COMMIT (all 12 waves): per active batch, wait for its B merges, replay the
 //                        batch in pod order against the exact current state (commit_spc_batch), export
-//                        the touched nodes, plan batch b + 2, publish Ctl::committed = b + 1.
-//   workgroup 1 + g      waves 0..7: SCORE -- the rows j = g (mod G) of this rank's nodes live in LDS for
-//                        the whole call; per batch wait for commit(b - 2), apply its export to the rows,
-//                        score 64 pods x the rows (lane = pod), fold the wave lists to one top-KC list per
-//                        pod, store it, arrive.
-//                        waves 8..15 (g < B only): MERGE pod g (g + G, ...) of every batch: wait for the G
-//                        arrivals, merge the G lists into the pod's K-entry Rec list [R > 1: exchange with
-//                        the peer ranks + rank merge], count the merge.
+//                        the touched nodes, plan batch b + kPipeLag, publish Ctl::committed = b + 1.
+//   workgroup 1 + g      SCORE (g < G, 12 waves): the rows j = g (mod G) of this rank's nodes live in LDS
+//                        for the whole call; per batch wait for commit(b - kPipeLag), apply its export to
+//                        the rows, score 64 pods x the rows (lane = pod; the screened scan), fold the wave
+//                        lists to one top-KC list per pod, store it, arrive.
+//   workgroup 1 + G + i  MERGE (kMS slots of kMT threads): slot id merges pods id, id + kMS M, ... of
+//                        every batch: wait for the G arrivals, merge the G lists into the pod's K-entry
+//                        Rec list [R > 1: exchange with the peer ranks + rank merge], count the merge.
 //
-// The two roles of a score workgroup run independent loops, so they never meet at s_barrier (which
-// would need every wave of the workgroup): each role synchronises its own waves through an LDS counter
-// (role_sync).  Every cross-workgroup hand-off is MI355X_MICROARCH "valid forms" row 1 (sc1 stores,
-// every storing wave drained, one lane's counter update; sc1 loads after the poll) and every wait is
-// bounded (PersistArgs::timeout_ticks -> error words 5..11).  Snapshot semantics: score(b) sees every
-// commit up to b - 2, commit(b) inherits b - 1's (oracle/cpu_ref.c or_schedule_pipelined).
+// The merger slots of a workgroup run independent loops, so they never meet at s_barrier: each slot
+// synchronises its own waves through an LDS counter (role_sync).  Every cross-workgroup hand-off is
+// MI355X_MICROARCH "valid forms" row 1 (sc1 stores, every storing wave drained, one lane's counter
+// update; sc1 loads after the poll) and every wait is bounded (PersistArgs::timeout_ticks -> error words
+// 5..11).  Snapshot semantics (lag kPipeLag = 3): score(b) sees every commit up to b - 3, commit(b)
+// inherits the nodes b - 2 and b - 1 committed (oracle/cpu_ref.c or_schedule_pipelined, lag 3).
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
@@ -267,7 +267,8 @@ static_assert(sizeof(MergeCtl) <= 64, "MergeCtl");
 
 constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16; }
 template <int K>
-constexpr size_t commit_total_bytes() { return commit_loc_bytes() + spc_lds_bytes<K, kPipeThreads>(); }
+constexpr size_t commit_total_bytes() { return commit_loc_bytes() + spc_lds_bytes<K, kPipeThreads, true>(); }
+static_assert(commit_total_bytes<16>() <= 160 * 1024, "the persistent commit's LDS (lag-3 slots)");
 
 // ------------------------------------------------------------------------------------------------
 // SCORE role (waves 0 .. kSW-1 of workgroup 1 + g)
@@ -313,7 +314,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     int64_t nact = 0;
     int idle = 0;
     for (int64_t b = 0;; ++b) {
-        // ---- wave 0: wait for commit(b-2), then ONE round of loads -- its plan for b, the cursor after it,
+        // ---- wave 0: wait for commit(b - kPipeLag), then ONE round of loads -- its plan for b, the cursor after it,
         // its export (count and entries, lane = entry) -- and apply the exported nodes this workgroup owns
         // to its LDS rows before the barrier (the other waves never touch the export) ----
         if (wave == 0) {
@@ -321,7 +322,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             if (lane == 0) {
                 unsigned long long seen = 0;
                 prog_at(P, g, b, kProgWaitCommit, 0);
-                if (b >= 2 && !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), &seen)) {
+                if (b >= kPipeLag &&
+                    !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - kPipeLag + 1), &seen)) {
                     set_err(P.err, 6);
                     prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
                     stop = 2;
@@ -332,14 +334,15 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             int64_t p0v = 0, donev = 0;
             int errv = 0, nxv = 0;
             uint64_t w0 = 0, w4 = 0, w5 = 0, w6 = 0;
-            const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= 2 ? b - 2 : 0) % 4) * P.xbuf_bytes);
+            const XBuf *xb =
+                reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= kPipeLag ? b - kPipeLag : 0) % 4) * P.xbuf_bytes);
             if (lane == 0) {
                 p0v = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
-                donev = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+                donev = b >= kPipeLag ? (int64_t)ld_coh(&ctl->cursor_at[(b - kPipeLag) % kPlanRing]) : 0;
                 // a failed peer (a wait timed out) ends the call for everyone
                 errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (b >= 2 && !stop) {
+            if (b >= kPipeLag && !stop) {
                 nxv = (int)(uint32_t)ld_coh(&xb->count);  // one address: one request for the wave
                 if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
                     const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[lane]);
@@ -373,10 +376,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         sync();
         if (pc->s_stop) return;
         const int64_t p0 = pc->s_p0;
-        if (pc->s_done >= NP) break;  // every pod resolved by commit(b-2) or earlier
+        if (pc->s_done >= NP) break;  // every pod resolved by commit(b - kPipeLag) or earlier
         if (p0 < 0 || p0 >= NP) {     // nothing planned for batch b (identical on every workgroup)
             if (tid == 0) prog_at(P, g, b, kProgIdle, (uint64_t)p0);
-            // a truncation re-plans within two batches; a longer run of empty plans is a protocol error
+            // a truncation re-plans within kPipeLag batches; a longer run of empty plans is a protocol error
             if (++idle > kPlanRing) {
                 if (tid == 0) set_err(P.err, 8);
                 return;
@@ -686,8 +689,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         }
         if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
-        Cand *part = P.part + (size_t)(b % 2) * part_elems * KC;
-        int64_t *part_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        Cand *part = P.part + (size_t)(b % kPipeLag) * part_elems * KC;  // merge(b) is done before score(b + kPipeLag)
+        int64_t *part_cnt = P.part_cnt + (size_t)(b % kPipeLag) * part_elems;
         if (folds && pl < P.B && p0 + pl < NP) {  // every lane of the group holds the pod's list: lane src stores entry src
             Cand *dst = part + ((size_t)pl * G + g) * KC;
             if (src < KC) {
@@ -757,14 +760,14 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
             int stop = 0;
             unsigned long long seen = 0;
             prog_at(P, slot_prog, b, kProgWaitCommit, 0);
-            if (b >= 2 && !spin_ge(P, slot_prog, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1),
-                                   &seen)) {
+            if (b >= kPipeLag && !spin_ge(P, slot_prog, &ctl->committed_x[g % kCtlReplicas].v,
+                                          (unsigned long long)(b - kPipeLag + 1), &seen)) {
                 set_err(P.err, 6);
                 prog_at(P, slot_prog, b, kProgWaitCommit | kProgTimedOut, seen);
                 stop = 2;
             }
             pc->m_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
-            pc->m_done = b >= 2 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 2) % kPlanRing]) : 0;
+            pc->m_done = b >= kPipeLag ? (int64_t)ld_coh(&ctl->cursor_at[(b - kPipeLag) % kPlanRing]) : 0;
             if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
             pc->m_stop = stop;
         }
@@ -800,8 +803,8 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         const size_t part_elems = (size_t)P.B * G;
         char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
         MergeArgs ma{};
-        ma.in = P.part + (size_t)(b % 2) * part_elems * KC;
-        ma.in_cnt = P.part_cnt + (size_t)(b % 2) * part_elems;
+        ma.in = P.part + (size_t)(b % kPipeLag) * part_elems * KC;
+        ma.in_cnt = P.part_cnt + (size_t)(b % kPipeLag) * part_elems;
         ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
         ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
         ma.p0_known = 1; ma.p0v = p0;
@@ -873,6 +876,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         loc.cursor = (int64_t)ld_rmw(&ctl->cursor);
         for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_rmw(&ctl->stats[i]);
         loc.xcount = 0;
+        loc.xcount2 = 0;
     }
     __syncthreads();
     const int cslot = P.G + P.B;  // progress slot
@@ -881,7 +885,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
     for (int64_t b = 0;; ++b) {
         const int64_t p0 = loc.plan[b % kPlanRing];  // written by this workgroup (or k_ctl_init)
         if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
-            // pods remain but nothing is planned: a truncation re-plans within two batches, so this is a
+            // pods remain but nothing is planned: a truncation re-plans within kPipeLag batches, so this is a
             // protocol error -- stop everyone instead of spinning
             if (threadIdx.x == 0) atomicCAS(P.err, 0, 9);
             if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
@@ -918,9 +922,11 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         ca.fc0 = reinterpret_cast<const int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
         ca.pods = P.pods; ca.ctl = ctl; ca.B = P.B;
         ca.plan = &ctl->plan[b % kPlanRing];
-        ca.plan1 = &ctl->plan[(b + 1) % kPlanRing];
-        ca.plan2 = &ctl->plan[(b + 2) % kPlanRing];
+        ca.plan1 = &ctl->plan[(b + kPipeLag - 1) % kPlanRing];
+        ca.plan2 = &ctl->plan[(b + kPipeLag) % kPlanRing];
+        // exports of b - 1 and b - 2 (ring slot 4 stays empty: the batches before the first)
         ca.xin = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes);
+        ca.xin2 = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 2 ? (b - 2) % 4 : 4) * P.xbuf_bytes);
         ca.xout = reinterpret_cast<XBuf *>(P.xring + (size_t)(b % 4) * P.xbuf_bytes);
         ca.out = P.out;
         ca.batch = b;
