@@ -53,6 +53,7 @@ struct SpcSmem {
     int32_t *hk;      // open-addressed table: node index per position (-1 = empty)
     int32_t *ps;      // prologue only (aliases S): slot of each inherited node's table position
     int64_t *s0;      // prologue only (aliases D): [inherited slot][3] state at this batch's score snapshot
+    double *iy;       // prologue only (aliases GS): [inherited slot][6] current state as doubles, reciprocals
     int32_t *HP;      // [K][64] table position of list entry (q, pod); kSpcInvalid for no entry
     uint32_t *tkc;    // [64] words: bit = position taken by a CONFIRMED touch (T)
     int32_t *ti;      // node index per slot
@@ -110,6 +111,15 @@ __device__ __forceinline__ void persist_plan(const CommitArgs &A, bool truncated
     if (nx >= A.pods.p) nx = -1;
     L->plan[(A.batch + kPipeLag) % kPlanRing] = nx;
     st_coh(A.plan2, (uint64_t)nx);
+}
+
+// a node state as the key needs it: the three doubles and their reciprocals (0 for a zero allocatable)
+__device__ __forceinline__ void stage_state(double *o, const int64_t *a) {
+    for (int r = 0; r < 3; ++r) {
+        const double f = (double)a[r];
+        o[r] = f;
+        o[3 + r] = recip_or_zero(a[r], f);
+    }
 }
 
 __device__ __forceinline__ void lds_order() {
@@ -222,6 +232,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.ps = reinterpret_cast<int32_t *>(m.S);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
         m.s0 = reinterpret_cast<int64_t *>(m.D);
+        m.iy = reinterpret_cast<double *>(m.GS);
     }
     const int nb = (int)((A.pods.p - p0 < A.B) ? A.pods.p - p0 : A.B);  // <= 64 (host-checked)
     // every wave: lane = pod j of the batch (lanes >= nb carry a zero request and are never read).
@@ -275,6 +286,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         for (int r = 0; r < 3; ++r) { m.s0[lane * 3 + r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
         x.labels = xi.labels; x.price = xi.price; x.pad = 0;
         m.ti[lane] = xi.idx;
+        stage_state(m.iy + lane * 6, xi.cur);
         const int h = spc_pos_insert(m.hk, xi.idx);
         if (LAG3) m.ps[h] = lane;
         atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
@@ -302,6 +314,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                     for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
                     x.labels = xi.labels; x.price = xi.price; x.pad = 0;
                     m.ti[e] = xi.idx;
+                    stage_state(m.iy + e * 6, xi.cur);
                     atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
                 }
             }
@@ -328,8 +341,11 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             const bool f0 = fits(rc, rm, rp, sel, x0[0], x0[1], x0[2], x.labels, LAB);
             const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
             dfl += (int)f1 - (int)f0;
-            const double k = lane_key<PRIO, DOM, LAB, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
-                                                           y3, x.price);
+            const double *yy = m.iy + t * 6;  // the slot's state as doubles and its reciprocals, staged once
+            double k;
+            const bool el = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
+                                                          yy[0], yy[1], yy[2], yy[3], yy[4], yy[5], y3, x.price, &k);
+            k = el ? k : -__builtin_inf();
             Srow[t] = k;
             const bool up = k != -__builtin_inf() && better(k, x.idx, pk, pi);
             pk = up ? k : pk; pi = up ? x.idx : pi; ps = up ? t : ps;
@@ -340,9 +356,16 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     }
 
     // ---- prologue part 2: the candidate lists (hash positions of their entries) ----
-    if (dbg) t_pre = __builtin_amdgcn_s_memtime() - t_start;
+    if (dbg) {
+        t_pre = __builtin_amdgcn_s_memtime() - t_start;
+        if (COH && lane == 0 && wave != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[9]), (unsigned long long)t_pre);
+    }
     if (!wait()) return false;  // a workgroup barrier when it waits
-    if (dbg) t_start = __builtin_amdgcn_s_memtime();
+    if (dbg) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        if (COH && tid == 0) A.dbg[7] += t - t_start;  // entry -> past the wait (wave 0)
+        t_start = t;
+    }
     if constexpr (COH) load_lists();
 #pragma unroll
     for (int u = 0; u < kHeadPer; ++u) {
@@ -751,7 +774,8 @@ constexpr size_t spc_lds_bytes() {
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
 // the prologue's aliases: the node -> slot map in S, the inherited snapshot states in D
-static_assert((size_t)64 * 129 * 8 >= kSpcHash * 4 && 64 * 64 >= 128 * 3 * 8, "SpcSmem prologue aliases");
+static_assert((size_t)64 * 129 * 8 >= kSpcHash * 4 && 64 * 64 >= 128 * 3 * 8 && 64 * kGS * 8 >= 128 * 6 * 8,
+              "SpcSmem prologue aliases");
 static_assert((size_t)(kSpcThreads / 64) * 64 * 16 >= kSpcHash * 4 && (kPipeThreads / 64) * 64 * 16 >= kSpcHash * 4,
               "SpcSmem::own aliases pbk/pbx");
 

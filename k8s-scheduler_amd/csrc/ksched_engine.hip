@@ -514,7 +514,7 @@ void print_persist_trace(ksched_ctx *c) {
     std::vector<uint64_t> t((size_t)c->trace_cap * kTraceCols);
     if (hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
-    double sum[14] = {};
+    double sum[16] = {};
     double scr[5] = {};  // WG 0 wave 0, screened batches: pass 1, bound merge, pass 2, exact phase (sums), exact rows
     int64_t nscr = 0;
     int64_t cnt = 0, first = -1, last = -1;
@@ -538,6 +538,8 @@ void print_persist_trace(ksched_ctx *c) {
         sum[11] += (double)(int64_t)(at(b, 9) - at(b, 8));     // WG 0: waiting for its slowest wave
         sum[12] += (double)(int64_t)(at(b, 10) - at(b, 9));    // WG 0: fold
         sum[13] += (double)(int64_t)(at(b, 5) - at(b, 10));    // WG 0: list stores + drain
+        sum[14] += (double)(int64_t)(at(b, 15) - at(b - 1, 4));  // commit(b-1) end -> commit loop top of b
+        sum[15] += (double)(int64_t)(at(b, 3) - at(b, 15));      // commit loop top -> past the merge wait
         if (at(b, 11) && at(b, 12)) {  // a screened batch (ksched_pipe.hip score_role)
             ++nscr;
             scr[0] += (double)(int64_t)(at(b, 11) - at(b, 0));
@@ -551,9 +553,9 @@ void print_persist_trace(ksched_ctx *c) {
         int64_t hd[16];
         if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14])
             fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f guess iterations/round %.2f failures %lld | "
-                    "cycles/batch: before the wait %.0f | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
+                    "cycles/batch: before the wait %.0f (other waves %.0f) entry to past the wait %.0f (poll %.0f, poll + barrier %.0f) | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
                     (long long)hd[14], (double)hd[12] / hd[14], (double)hd[5] / std::max<int64_t>(1, hd[12]),
-                    (long long)hd[13], (double)hd[6] / hd[14], (double)hd[0] / hd[14],
+                    (long long)hd[13], (double)hd[6] / hd[14], (double)hd[9] / hd[14] / 11.0, (double)hd[7] / hd[14], (double)hd[10] / hd[14], (double)hd[11] / hd[14], (double)hd[0] / hd[14],
                     (double)hd[1] / hd[14], (double)hd[2] / hd[14], (double)hd[3] / hd[14], (double)hd[4] / hd[14]);
     }
     if (c->d_mdbg) {
@@ -569,10 +571,10 @@ void print_persist_trace(ksched_ctx *c) {
     const double us = 0.01 / (double)cnt;  // 100 MHz ticks -> us, mean
     fprintf(stderr,
             "persist trace: %lld batches, period %.2f us | to-score %.2f score %.2f merge %.2f to-commit %.2f "
-            "commit %.2f commit-gap %.2f | wg0: poll %.2f apply %.2f score %.2f (rows %.2f slowest-wave %.2f fold %.2f "
-            "stores %.2f) | merger poll %.2f\n",
+            "commit %.2f commit-gap %.2f (to loop top %.2f, top to past the wait %.2f) | wg0: poll %.2f apply %.2f "
+            "score %.2f (rows %.2f slowest-wave %.2f fold %.2f stores %.2f) | merger poll %.2f\n",
             (long long)cnt, 0.01 * (double)(int64_t)(at(last, 4) - at(first, 4)) / (double)std::max<int64_t>(1, last - first),
-            sum[0] * us, sum[1] * us, sum[2] * us, sum[3] * us, sum[4] * us, sum[5] * us, sum[6] * us, sum[7] * us,
+            sum[0] * us, sum[1] * us, sum[2] * us, sum[3] * us, sum[4] * us, sum[5] * us, sum[14] * us, sum[15] * us, sum[6] * us, sum[7] * us,
             sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
     if (nscr)
         fprintf(stderr, "persist screen (WG 0 wave 0): %lld of %lld batches screened | pass 1 %.2f us, bound %.2f us, "

@@ -76,6 +76,16 @@ __device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const un
     return poll_ge(p, v, P.timeout_ticks, &P.ctl->polls_rmw, seen, P.prog ? P.prog + kProgWords * slot + 2 : nullptr);
 }
 
+// A counter read ahead of its wait (its latency hides behind other work).  KSCHED_EARLY_RMW: as an atomic
+// read-modify-write, which is served at the coherence point instead of by a possibly stale L2 line.
+__device__ __forceinline__ unsigned long long early_read(const unsigned long long *p) {
+#ifdef KSCHED_EARLY_RMW
+    return (unsigned long long)ld_rmw(p);
+#else
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
 // the first failure names the wait that timed out (ksched_sync reports it)
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
@@ -245,7 +255,9 @@ struct ScoreLayout {
     __host__ __device__ static size_t total_screen(int R) { return total(R) + (size_t)R * 16; }
     // ... and pass 1's per-pair records for pass 2: [kSW][ceil(R / kSW)][64] f16
     __host__ __device__ static size_t hrec_off(int R) { return total_screen(R); }
-    __host__ __device__ static size_t hrec_bytes(int R) { return (size_t)kSW * ((R + kSW - 1) / kSW) * 64 * 2; }
+    // rows per wave, rounded up to pairs (pass 1 stores the records of two rows in one 32-bit word)
+    __host__ __device__ static int hrec_qw(int R) { return ((R + kSW - 1) / kSW + 1) / 2 * 2; }
+    __host__ __device__ static size_t hrec_bytes(int R) { return (size_t)kSW * hrec_qw(R) * 64 * 2; }
     __host__ __device__ static size_t total_with_hrec(int R) { return total_screen(R) + hrec_bytes(R); }
 };
 
@@ -280,7 +292,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     NodeRec *rows = reinterpret_cast<NodeRec *>(smem + ScoreLayout<KC, K>::rows_off());
     char *fold = smem + ScoreLayout<KC, K>::fold_off(R);
     float4 *ysq = reinterpret_cast<float4 *>(smem + ScoreLayout<KC, K>::ysq_off(R));  // screen reciprocals, SoA rows
-    uint16_t *hrec = reinterpret_cast<uint16_t *>(smem + ScoreLayout<KC, K>::hrec_off(R));  // [kSW][QW][64] (P.screen_h)
+    uint16_t *hrec = reinterpret_cast<uint16_t *>(smem + ScoreLayout<KC, K>::hrec_off(R));  // [kSW][QW/2][64] u16 pairs (P.screen_h)
     int32_t *s_cnt = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 12);  // [64], after the fold lists
     constexpr int kST = kSW * 64;
     const int tid = threadIdx.x;
@@ -313,6 +325,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
     int64_t nact = 0;
     int idle = 0;
+    unsigned long long early_c = 0;  // wave 0 lane 0: Ctl::committed as read before the last fold
     for (int64_t b = 0;; ++b) {
         // ---- wave 0: wait for commit(b - kPipeLag), then ONE round of loads -- its plan for b, the cursor after it,
         // its export (count and entries, lane = entry) -- and apply the exported nodes this workgroup owns
@@ -321,12 +334,16 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             int stop = 0;
             if (lane == 0) {
                 unsigned long long seen = 0;
-                prog_at(P, g, b, kProgWaitCommit, 0);
-                if (b >= kPipeLag &&
-                    !spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - kPipeLag + 1), &seen)) {
-                    set_err(P.err, 6);
-                    prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
-                    stop = 2;
+                const unsigned long long need = (unsigned long long)(b - kPipeLag + 1);
+                // the count read before the previous batch's fold (early_c) usually suffices: no wait, and no
+                // progress store ahead of this round of loads
+                if (b >= kPipeLag && early_c < need) {
+                    prog_at(P, g, b, kProgWaitCommit, 0);
+                    if (!spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, need, &seen)) {
+                        set_err(P.err, 6);
+                        prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
+                        stop = 2;
+                    }
                 }
                 if (g == 0) trace_at(P, b, 6);
             }
@@ -416,7 +433,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             const int Rv = (int)((n - g + G - 1) / G);  // rows of this workgroup that hold a node
             const int QW = (R + kSW - 1) / kSW;
             const bool keep_h = P.screen_h != 0;      // pass 1 leaves a record per pair for pass 2
-            uint16_t *hw = hrec + (size_t)wave * QW * 64 + lane;
+            // the records of a wave's rows k (r = wave + k kSW): rows 2i and 2i + 1 share a 32-bit word per lane
+            uint32_t *hw = reinterpret_cast<uint32_t *>(hrec) + (size_t)wave * (ScoreLayout<KC, K>::hrec_qw(R) / 2) * 64 + lane;
             // One row for every pod of the batch: the f32 fractions decide the predicate unless one lies
             // within 2^-20 of 1 or is NaN (then the int64 compares of the row decide, for every pod); the
             // screen value, whether it bounds an eligible key from below, and whether the pair has a key.
@@ -448,6 +466,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 // branch-free: a pair whose fraction is ambiguous (within 2^-20 of 1, or NaN) contributes no
                 // bound, gets a NaN record (scored exactly if it can matter) and its predicate is counted
                 // exactly after the loop, from its row's int64 values
+                static_assert(kSPU % 2 == 0, "pass 1 stores the records of row pairs");
                 for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
                     float4 yv[kSPU];
                     uint64_t lb[kSPU];
@@ -458,6 +477,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         lb[u] = LAB ? rows[r < Rv ? r : r0].labels : 0ull;
                     }
                     uint32_t xs[kSPU];
+                    uint32_t hh[kSPU];
+                    uint32_t ambm = 0;  // rows of this group with an ambiguous fraction for this lane's pod
 #pragma unroll
                     for (int u = 0; u < kSPU; ++u) {
                         const int r = r0 + u * kSW;
@@ -475,12 +496,21 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         // (f16 rounding is within 2^-11 relative); +inf (never needed) without a key; NaN stays NaN
                         const float w = 10.0f - v;
                         const float wd = w - __builtin_fabsf(w) * 0x1p-10f - 0x1p-24f;
-                        if (valid)
-                            hw[(size_t)(r / kSW) * 64] =
-                                __half_as_ushort(__float2half_rn(amb ? __builtin_nanf("") : (el ? wd : __builtin_inff())));
-                        const bool anya = __ballot(valid && amb) != 0;
-                        if (lane == 0 && na < QW) arow[wave * QW + na] = (uint16_t)r;  // kept when anya
-                        na += anya ? 1 : 0;
+                        hh[u] = __half_as_ushort(__float2half_rn(amb ? __builtin_nanf("") : (el ? wd : __builtin_inff())));
+                        ambm |= (valid && amb) ? 1u << u : 0u;
+                    }
+                    // the records of rows k, k + 1 (k = (r0 - wave) / kSW + u, u even) in one store; a pair's second
+                    // row past the wave's last is never read
+#pragma unroll
+                    for (int u = 0; u < kSPU; u += 2)
+                        if (r0 + u * kSW < Rv) hw[(size_t)(((r0 - wave) / kSW + u) / 2) * 64] = hh[u] | (hh[u + 1] << 16);
+                    if (__ballot(ambm != 0)) {  // wave-uniform, rare: queue the rows with an ambiguous pair
+#pragma unroll
+                        for (int u = 0; u < kSPU; ++u) {
+                            const bool anya = __ballot((ambm >> u) & 1u) != 0;
+                            if (lane == 0 && na < QW) arow[wave * QW + na] = (uint16_t)(r0 + u * kSW);  // kept when anya
+                            na += anya ? 1 : 0;
+                        }
                     }
 #pragma unroll
                     for (int u = 0; u < kSPU; ++u) {
@@ -557,7 +587,11 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 for (int i0 = 0; i0 < nr; i0 += 8) {
                     uint16_t hv[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) hv[u] = hw[(size_t)(i0 + u < nr ? i0 + u : i0) * 64];
+                    for (int u = 0; u < 8; u += 2) {
+                        const uint32_t x = hw[(size_t)((i0 + u < nr ? i0 + u : i0) / 2) * 64];
+                        hv[u] = (uint16_t)x;
+                        hv[u + 1] = (uint16_t)(x >> 16);
+                    }
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         const float vd = 10.0f - __half2float(__ushort_as_half(hv[u]));
@@ -651,6 +685,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         }
         if (g == 0 && tid == 0) trace_at(P, b, 8);
         const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
+        // the commit count for the next batch's wait, read now: its latency hides behind the fold and stores
+        if (tid == 0) early_c = early_read(&ctl->committed_x[g % kCtlReplicas].v);
         sync();  // every wave's scan is done (the fold area is free); s_cnt was zeroed
         if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
@@ -891,26 +927,38 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
             if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
             return;
         }
+        if (threadIdx.x == 0) trace_at(P, b, 15);
         LanePods pre{0, 0, 0, 0};
         const bool act = p0 >= 0 && p0 < P.pods.p;
+        constexpr int kPoller = 128;  // wave 2 lane 0: its wave loads nothing else in the prologue
+        unsigned long long early_m = 0;
         if (act) {
             idle = 0;
             ++nact;
             // the pods' requests are known now: their loads overlap the inherited-slot work
             if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
+            // the merge count, read now: its latency hides behind the prologue (the merges are usually done)
+            if (threadIdx.x == kPoller)
+                early_m = early_read(&ctl->merged[(nact - 1) % 4].v);
         }
         // the batch's merges (everything of the commit that needs no candidate list runs before this)
         auto wait_merged = [&]() -> bool {
             if (act) {
-                if (threadIdx.x == 0) {
+                const uint64_t tw0 = P.cdbg ? __builtin_amdgcn_s_memtime() : 0;
+                if (threadIdx.x == kPoller) {
                     const int slot = (int)((nact - 1) % 4);
                     const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
                     unsigned long long seen = 0;
-                    prog_at(P, cslot, b, kProgWaitMerged, 0);
-                    s_stop = poll_ge(&ctl->merged[slot].v, want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
-                    if (s_stop) prog_at(P, cslot, b, kProgWaitMerged | kProgTimedOut, seen);
+                    s_stop = 0;
+                    if (early_m < want) {
+                        prog_at(P, cslot, b, kProgWaitMerged, 0);
+                        s_stop = poll_ge(&ctl->merged[slot].v, want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
+                        if (s_stop) prog_at(P, cslot, b, kProgWaitMerged | kProgTimedOut, seen);
+                    }
+                    if (P.cdbg) P.cdbg[10] += __builtin_amdgcn_s_memtime() - tw0;  // the poll
                 }
                 __syncthreads();
+                if (P.cdbg && threadIdx.x == 0) P.cdbg[11] += __builtin_amdgcn_s_memtime() - tw0;  // poll + barrier
                 if (s_stop) return false;
             }
             if (threadIdx.x == 0) trace_at(P, b, 3);
