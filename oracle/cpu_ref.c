@@ -786,3 +786,84 @@ int or_schedule_pipelined(const or_opts *o, int32_t K, int32_t B, int64_t n,
     free(recs); free(fc);
     return OR_OK;
 }
+
+/* The persistent pipeline at lag L (2 <= L <= 4; the device runs L = 3, ksched_pipe.hip): batch b is
+ * scored against the node state after commit(b - L); commit(b) inherits the nodes committed by batches
+ * b - L + 1 .. b - 1, each with its state at b's snapshot (the start state of the oldest of those batches
+ * that committed it) and its current state (after the newest); plan(b) for b < L is b * B, commit(b)
+ * plans batch b + L (its cursor after a truncation, else plan(b + L - 1) + B), and a batch whose plan is
+ * not the cursor is skipped.  Test infrastructure: tests/test_oracle.py checks it against or_schedule. */
+int or_schedule_lagged(const or_opts *o, int32_t K, int32_t B, int32_t L, int64_t n,
+                       int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
+                       int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
+                       int32_t *out_idx, double *out_score, int32_t *out_feas, int64_t *stats)
+{
+    enum { RING = 8 };
+    or_xrec *X[RING], *inh;
+    int32_t nx[RING];
+    int64_t plan[RING];
+    or_rec *recs;
+    int64_t *fc;
+    int64_t cursor = 0, b;
+    int k;
+    if (K < 1 || B < 1 || L < 2 || L > 4) return OR_E_INVALID;
+    for (k = 0; k < RING; k++) { X[k] = (or_xrec *)malloc(sizeof(or_xrec) * (size_t)(B + 1)); nx[k] = 0; plan[k] = -1; }
+    inh = (or_xrec *)malloc(sizeof(or_xrec) * (size_t)(L * B + 1));
+    recs = (or_rec *)malloc(sizeof(or_rec) * (size_t)K * (size_t)B);
+    fc = (int64_t *)malloc(sizeof(int64_t) * (size_t)B);
+    for (k = 0; k < L; k++) plan[k] = (int64_t)k * B < p ? (int64_t)k * B : -1;
+    if (stats) stats[0] = stats[1] = stats[2] = 0;
+    for (b = 0; cursor < p; b++) {
+        const int cb = (int)(b % RING);
+        int64_t s = plan[cb], nb, done, i, nxt;
+        int32_t nin = 0, t;
+        int d;
+        if (b >= L) { /* score(b) sees commit(b - L) */
+            const int ab = (int)((b - L) % RING);
+            for (i = 0; i < nx[ab]; i++) {
+                const int32_t j = X[ab][i].idx;
+                ac[j] = X[ab][i].cur[0]; am[j] = X[ab][i].cur[1]; ap[j] = X[ab][i].cur[2];
+            }
+        }
+        nx[cb] = 0;
+        nb = (s >= 0 && s < p) ? (p - s < B ? p - s : B) : 0;
+        if (nb > 0) or_local_topk(o, K, 0, n, ac, am, ap, labels, price, nb, rc + s, rm + s, rp + s,
+                                  sel ? sel + s : NULL, recs, fc);
+        if (nb == 0 || s != cursor) {
+            if (nb > 0 && stats) stats[2]++; /* invalidated speculation */
+            nxt = plan[(b + L - 1) % RING];
+            plan[(b + L) % RING] = nxt < 0 || nxt + B >= p ? -1 : nxt + B;
+            continue;
+        }
+        /* inherited: newest export first; an older export's entry for a node already present only
+         * moves that node's snapshot state back to the older start state */
+        for (d = 1; d < L && b - d >= 0; d++) {
+            const int xb = (int)((b - d) % RING);
+            for (i = 0; i < nx[xb]; i++) {
+                for (t = 0; t < nin && inh[t].idx != X[xb][i].idx; t++) {}
+                if (t == nin) inh[nin++] = X[xb][i];
+                else memcpy(inh[t].sb, X[xb][i].sb, sizeof(inh[t].sb));
+            }
+        }
+        done = commit_inherit(o, K, nb, rc + s, rm + s, rp + s, sel ? sel + s : NULL, recs, fc, inh, nin,
+                              X[cb], &nx[cb], out_idx + s, out_score + s, out_feas + s);
+        cursor = s + done;
+        nxt = plan[(b + L - 1) % RING];
+        nxt = done < nb ? cursor : (nxt < 0 ? -1 : nxt + B);
+        plan[(b + L) % RING] = nxt >= p ? -1 : nxt;
+        if (stats) { stats[0]++; stats[1] += done < nb; }
+    }
+    /* drain: the commits the last batches' scores never saw */
+    for (k = L; k >= 1; k--) {
+        int64_t i;
+        const int ab = (int)((b - k) % RING);
+        if (b - k < 0) continue;
+        for (i = 0; i < nx[ab]; i++) {
+            const int32_t j = X[ab][i].idx;
+            ac[j] = X[ab][i].cur[0]; am[j] = X[ab][i].cur[1]; ap[j] = X[ab][i].cur[2];
+        }
+    }
+    for (k = 0; k < RING; k++) free(X[k]);
+    free(inh); free(recs); free(fc);
+    return OR_OK;
+}

@@ -157,3 +157,35 @@ def test_pipelined_restatement_edge_clusters(oracle_mod, seed):
         assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
         for a, b in zip(st, bst):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("lag", [2, 3, 4])
+@pytest.mark.parametrize("name,nn,pp,K,B", [("c2", 800, 700, 4, 32), ("c3", 1500, 600, 8, 64),
+                                            ("c5", 2000, 700, 16, 64), ("c3", 700, 500, 4, 64)])
+def test_lagged_restatement_equals_sequential(oracle_mod, name, nn, pp, K, B, lag):
+    """The persistent pipeline at lag 2, 3 (the device's) and 4: score(b) against commit(b - lag), commit(b)
+    inheriting the exports of b - lag + 1 .. b - 1 with the oldest start state as snapshot state."""
+    from ksched import cluster
+    cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, K, B, lag)
+    assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+    assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+    for a, b in zip(st, bst):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_lagged_restatement_edge_clusters(oracle_mod, seed):
+    """Small adversarial clusters (high conflict: many truncations, skips and re-plans) at lag 3."""
+    from ksched import cluster
+    combos = [(0, 0, False), (0, 1, False), (1, 1, False), (0, 1, True), (1, 1, True), (0, 0, True)]
+    pr, dm, lb = combos[seed]
+    cl = cluster.random_small(91 + seed, n_nodes=96, n_pods=500, priority=pr, domain=dm, use_labels=lb)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    for K, B in ((4, 16), (8, 64), (16, 64)):
+        bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, K, B, 3)
+        assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+        assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+        for a, b in zip(st, bst):
+            assert np.array_equal(a, b)
