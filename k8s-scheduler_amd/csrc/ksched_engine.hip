@@ -553,9 +553,9 @@ void print_persist_trace(ksched_ctx *c) {
         int64_t hd[16];
         if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14])
             fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f guess iterations/round %.2f failures %lld | "
-                    "cycles/batch: before the wait %.0f (other waves %.0f) entry to past the wait %.0f (poll %.0f, poll + barrier %.0f) | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
+                    "cycles/batch: before the wait %.0f (other waves %.0f) entry to past the wait %.0f (poll %.0f, poll + barrier %.0f, early read sufficed %.3f) | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
                     (long long)hd[14], (double)hd[12] / hd[14], (double)hd[5] / std::max<int64_t>(1, hd[12]),
-                    (long long)hd[13], (double)hd[6] / hd[14], (double)hd[9] / hd[14] / 11.0, (double)hd[7] / hd[14], (double)hd[10] / hd[14], (double)hd[11] / hd[14], (double)hd[0] / hd[14],
+                    (long long)hd[13], (double)hd[6] / hd[14], (double)hd[9] / hd[14] / 11.0, (double)hd[7] / hd[14], (double)hd[10] / hd[14], (double)hd[11] / hd[14], (double)hd[15] / hd[14], (double)hd[0] / hd[14],
                     (double)hd[1] / hd[14], (double)hd[2] / hd[14], (double)hd[3] / hd[14], (double)hd[4] / hd[14]);
     }
     if (c->d_mdbg) {

@@ -395,9 +395,6 @@ __device__ __forceinline__ uint32_t hw_where() {
     return (xcc & 0xf) << 8 | ((hw >> 13) & 7) << 4 | ((hw >> 8) & 0xf);
 }
 __device__ __forceinline__ void prog_at(const PersistArgs &P, int slot, int64_t b, int phase, uint64_t seen) {
-#ifdef KSCHED_NO_PROG
-    return;
-#endif
     if (!P.prog) return;
     __hip_atomic_store(P.prog + kProgWords * slot, (uint64_t)b << 8 | (uint64_t)phase, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);

@@ -76,16 +76,6 @@ __device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const un
     return poll_ge(p, v, P.timeout_ticks, &P.ctl->polls_rmw, seen, P.prog ? P.prog + kProgWords * slot + 2 : nullptr);
 }
 
-// A counter read ahead of its wait (its latency hides behind other work).  KSCHED_EARLY_RMW: as an atomic
-// read-modify-write, which is served at the coherence point instead of by a possibly stale L2 line.
-__device__ __forceinline__ unsigned long long early_read(const unsigned long long *p) {
-#ifdef KSCHED_EARLY_RMW
-    return (unsigned long long)ld_rmw(p);
-#else
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-
 // the first failure names the wait that timed out (ksched_sync reports it)
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
@@ -686,7 +676,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (g == 0 && tid == 0) trace_at(P, b, 8);
         const uint64_t t_scan = (P.trace && tid == 0) ? wall_clock64() : 0;
         // the commit count for the next batch's wait, read now: its latency hides behind the fold and stores
-        if (tid == 0) early_c = early_read(&ctl->committed_x[g % kCtlReplicas].v);
+        if (tid == 0) early_c = __hip_atomic_load(&ctl->committed_x[g % kCtlReplicas].v, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
         sync();  // every wave's scan is done (the fold area is free); s_cnt was zeroed
         if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
@@ -939,7 +930,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
             if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
             // the merge count, read now: its latency hides behind the prologue (the merges are usually done)
             if (threadIdx.x == kPoller)
-                early_m = early_read(&ctl->merged[(nact - 1) % 4].v);
+                early_m = __hip_atomic_load(&ctl->merged[(nact - 1) % 4].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // the batch's merges (everything of the commit that needs no candidate list runs before this)
         auto wait_merged = [&]() -> bool {
@@ -950,6 +941,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
                     const unsigned long long want = (unsigned long long)((nact - 1) / 4 + 1) * (unsigned long long)P.B;
                     unsigned long long seen = 0;
                     s_stop = 0;
+                    if (P.cdbg && early_m >= want) P.cdbg[15] += 1;  // diagnostics: the early read sufficed
                     if (early_m < want) {
                         prog_at(P, cslot, b, kProgWaitMerged, 0);
                         s_stop = poll_ge(&ctl->merged[slot].v, want, P.timeout_ticks, &ctl->polls_rmw, &seen) ? 0 : 1;
