@@ -220,8 +220,9 @@ struct CommitArgs {
     int32_t release;        // COH: also write back the XCD's L2 (agent release) before Ctl::committed
 };
 
-// Commit(b) -> score(b+2) hand-off on the device: the committing wave drains its stores, writes back the
-// XCD L2 (agent release) and publishes Ctl::committed = b + 1; score(b+2) polls it instead of waiting
+// Commit(b) -> score(b + lag) hand-off on the device (lag 2 on the stream pipeline, kPipeLag in k_pipe): the
+// committing wave drains its stores, writes back the XCD L2 (agent release) and publishes
+// Ctl::committed = b + 1; the later score polls it instead of waiting
 // on a cross-queue stream event (~12 us per hand-off).  Call from ONE wave that
 // made every global store of the commit (the others made none).
 // COH (persistent pipeline): every handed-off store was an sc1 store, so no L2 write-back is needed.
