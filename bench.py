@@ -74,7 +74,6 @@ def parse():
                     help="skip the (untimed) prefix check of the timed run's results against the CPU oracle")
     ap.add_argument("--check-pods", type=int, default=5000)
     ap.add_argument("--no-xchg", action="store_true", help="N > 1: RCCL stream pipeline instead of the device-side exchange")
-    ap.add_argument("--same-device", action="store_true", help=argparse.SUPPRESS)  # N > 1 rehearsal on one GPU
     return ap.parse_args()
 
 
@@ -142,19 +141,12 @@ def main():
     if world != args.gpus and args.gpus > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dist = None
-    if args.same_device:
-        # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, each grid on its share of
-        # the CUs, torch.distributed over gloo, no RCCL communicator (RCCL refuses two ranks per GPU)
-        local = 0
-    tdev = "cpu" if args.same_device else "cuda"
+    tdev = "cuda"
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        if args.same_device:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import torch
 
     cl = cluster.make_cluster(args.config, n_nodes=args.nodes, n_pods=args.pods)
@@ -164,9 +156,7 @@ def main():
     # N > 1: the persistent pipeline with the device-side exchange over xGMI (ksched_xchg_*), the RCCL
     # communicator kept as the fallback transport (stream pipeline, one all-gather per batch)
     eng, (lo, hi) = make_sharded_engine(cl, rank, world, device=local, mode=mode, topk=args.topk,
-                                        batch=args.batch, timing=False, xchg=world > 1 and not args.no_xchg,
-                                        comm=not args.same_device,
-                                        pipe_wgs=(256 - 8) // world if args.same_device else 0)
+                                        batch=args.batch, timing=False, xchg=world > 1 and not args.no_xchg)
     eng.save_state()
     eng.upload_pods(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
 

@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 4
+#define KSCHED_ABI_VERSION 5
 
 /* status codes */
 #define KSCHED_OK 0
@@ -147,6 +147,13 @@ int ksched_xchg_ready(const ksched_ctx *ctx);
 /* Turns the exchange off on this rank (later batched calls take the RCCL path).  Every rank calls it when
  * any rank failed to import (ABI 4): the ranks must agree on the transport. */
 int ksched_xchg_close(ksched_ctx *ctx);
+/* Ranks as threads of ONE process on ONE device (ABI 5): joins ctxs[0..n-1] (rank r at ctxs[r], each created
+ * with nranks = n, 2 <= n <= 4, batch <= 64 and the same options) into the device exchange without IPC.  Their
+ * persistent pipelines then run as ONE cooperative launch -- rank r's workgroups a contiguous block range, the
+ * ranks sharing the CUs equally -- so every rank's grid is resident at once by construction; separate launches
+ * (of separate processes) sharing a device guarantee no such thing.  The contexts' threads
+ * call ksched_run concurrently, as with ksched_set_group; destroy all of them together. */
+int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n);
 
 typedef struct ksched_group ksched_group;
 int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out);

@@ -12,6 +12,11 @@
  *          on a failed bind of pod i: the reference leaves pod i unbound and every later pod re-reads
  *          a cluster WITHOUT it, so the engine's commits of pods i.. (none bound yet) are undone with
  *          ksched_apply_delta and the pods after i are scheduled again: start = i + 1
+ *   then the bound-pod watch events (the shim's onPodEvent): ADDED of a pod bound by another scheduler
+ *          charges its node, DELETED of a bound pod frees it (ksched_apply_delta); ADDED of a pod this run
+ *          bound is skipped (already committed); a pod bound to a node missing from the node list ends
+ *          the program with KSCHED_E_UNKNOWN_NODE, as the reference's usedResource panics there
+ *          (anchor/predicate.go:94-99)
  *
  * Input (argv[1]) and output (argv[2]) are flat little-endian files written / read by
  * tests/test_gpu_integration.py; argv[3..]: mode, topk, batch.  The "API server" is simulated: a bind
@@ -40,18 +45,19 @@ int main(int argc, char **argv) {
     }
     FILE *in = fopen(argv[1], "rb");
     if (!in) { perror("input"); return 1; }
-    int64_t hdr[7]; /* n, p, nfail, priority, domain, use_labels, has_price */
+    int64_t hdr[8]; /* n, p, nfail, priority, domain, use_labels, has_price, nevents */
     if (read_all(in, hdr, sizeof(hdr))) { fprintf(stderr, "bad header\n"); return 1; }
-    const int64_t n = hdr[0], p = hdr[1], nfail = hdr[2];
+    const int64_t n = hdr[0], p = hdr[1], nfail = hdr[2], nev = hdr[7];
     int64_t *ac = malloc(8 * n), *am = malloc(8 * n), *ap = malloc(8 * n);
     uint64_t *lab = malloc(8 * n);
     float *price = malloc(4 * n);
     int64_t *rc = malloc(8 * p), *rm = malloc(8 * p), *rp = malloc(8 * p);
     uint64_t *sel = malloc(8 * p);
     int64_t *failset = malloc(8 * (nfail + 1));
+    int64_t *ev = malloc(8 * 5 * (nev + 1)); /* {type 1 ADDED | 2 DELETED, node (-1: not in the node list), cpu, mem, ours} */
     if (read_all(in, ac, 8 * n) || read_all(in, am, 8 * n) || read_all(in, ap, 8 * n) || read_all(in, lab, 8 * n) ||
         read_all(in, price, 4 * n) || read_all(in, rc, 8 * p) || read_all(in, rm, 8 * p) || read_all(in, rp, 8 * p) ||
-        read_all(in, sel, 8 * p) || read_all(in, failset, 8 * nfail)) {
+        read_all(in, sel, 8 * p) || read_all(in, failset, 8 * nfail) || read_all(in, ev, 8 * 5 * nev)) {
         fprintf(stderr, "short input\n");
         return 1;
     }
@@ -117,6 +123,20 @@ int main(int argc, char **argv) {
         }
         if (resume < 0) break;
         start = resume;
+    }
+    /* the bound-pod watch (integration/anchor_ksched.go onPodEvent) */
+    for (int64_t e = 0; e < nev; ++e) {
+        const int64_t *x = ev + 5 * e;
+        if (x[0] == 1 && x[4]) continue; /* ADDED for a pod this run bound: committed by ksched_schedule */
+        if (x[1] < 0) {
+            fprintf(stderr, "ksched_driver: watch event %lld: pod bound to an unknown node (%d)\n", (long long)e,
+                    KSCHED_E_UNKNOWN_NODE);
+            exit(-KSCHED_E_UNKNOWN_NODE);
+        }
+        const int64_t sign = x[0] == 2 ? 1 : -1; /* bound: used += (cpu, mem, 1), allocatable -= ... */
+        const int32_t j = (int32_t)x[1];
+        const int64_t dc = sign * x[2], dm = sign * x[3], dp = sign;
+        if ((rcode = ksched_apply_delta(ctx, 1, &j, &dc, &dm, &dp)) != KSCHED_OK) die(ctx, "ksched_apply_delta", rcode);
     }
     int64_t *fc = malloc(8 * n), *fm = malloc(8 * n), *fp = malloc(8 * n);
     if ((rcode = ksched_read_nodes(ctx, n, fc, fm, fp)) != KSCHED_OK) die(ctx, "ksched_read_nodes", rcode);

@@ -8,7 +8,7 @@
 //   1. (wave 0, integer work only) GUESSES every remaining pod's placement: its first list entry that
 //      is neither touched nor guessed by an earlier pod of the round ("first touch"), or none when the
 //      pod has no feasible node or its list is exhausted;
-//   2. (all 16 waves) evaluates the guesses in parallel: for every guessed node, its state after the
+//   2. (all waves: 8 in k_commit_spc, 12 in the persistent commit) evaluates the guesses in parallel: for every guessed node, its state after the
 //      guessing pod's commit, and every pod's exact key and predicate delta against that state;
 //   3. (wave 0, lane = pod) checks each pod's exact sequential decision under the guesses of the pods
 //      before it: fc = predicate count, t* = best touched node (confirmed + guessed before it), u* =
@@ -67,8 +67,8 @@ struct SpcSmem {
     int32_t *gn;      // per pod: guessed node (>= 0), -1 list exhausted, -2 predicted no fit
     int32_t *gq;      // per pod: list position of the guess
     int32_t *gs;      // per pod: slot of the guess
-    double *pbk;      // [16 waves][64 pods] partial best key over the wave's guessed columns
-    int64_t *pbx;     // [16 waves][64 pods] (slot << 32) | node of that best
+    double *pbk;      // [waves][64 pods] partial best key over the wave's guessed columns
+    int64_t *pbx;     // [waves][64 pods] (slot << 32) | node of that best
     int32_t *ctl;     // [0] round start c, [1] window end, [2] stop
     int32_t *own;     // [kSpcHash] lowest pod proposing each position in a guess iteration (64 = none);
                       // step 1 only (aliases pbk/pbx, which steps 2-3 use)
@@ -189,7 +189,9 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         if (wave == 0) {
             if (lane == 0) {
                 if (COH) {
-                    st_coh(&A.xout->count, 0ull);
+                    // an empty export is never written: the slot keeps an older batch's tag, which score(b + 3)
+                    // reads as empty.  (An idle commit -- plan -1 -- does not wait for any merge, so a store here
+                    // could land under a score workgroup still reading the slot's previous export: ADVICE r3.)
                     L->xcount2 = L->xcount;
                     L->xcount = 0;
                     if (p0 >= 0 && p0 < A.pods.p) st_coh(&A.ctl->stats[3], (uint64_t)++L->stats[3]);
@@ -737,7 +739,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     }
     if (lane == 0) {
         if (COH) {
-            st_coh(&A.xout->count, (uint64_t)(uint32_t)base);
+            st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
             L->xcount2 = L->xcount;
             L->xcount = base;
             L->cursor = p0 + done;

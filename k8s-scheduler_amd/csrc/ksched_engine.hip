@@ -12,6 +12,7 @@
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <cstdio>
 #include <cstdlib>
@@ -40,7 +41,58 @@ struct ksched_group {
     uint64_t gen = 0;
 };
 
+// Ranks of ONE process sharing ONE device, joined by ksched_xchg_join_local: the device exchange of the
+// node-sharded persistent pipeline without IPC, and their persistent kernels as ONE cooperative launch
+// (k_pipe over a PipeLaunch of every rank's arguments), so every rank's grid is resident at once by
+// construction.  Per call the ranks meet twice on the host: to agree on FAST53, and to launch -- the last
+// rank to arrive issues the launch on its stream behind every rank's pre-launch work (events) and the others'
+// streams wait for it.
+struct ksched_lgroup {
+    int R = 0, dev = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool broken = false;        // a rank never arrived: the group is unusable
+    int acc = 0, result = 0;    // FAST53 agreement
+    PipeLaunch L{};             // the staged launch (rank r's arguments in L.P[r])
+    hipStream_t stream[kMaxLocalRanks] = {};
+    hipEvent_t ready[kMaxLocalRanks] = {};
+    hipEvent_t done = nullptr;
+    int kc = 0, k = 0, prio = 0, dom = 0;
+    bool lab = false, f53 = false;
+    hipError_t launch_err = hipSuccess;
+    ~ksched_lgroup() {
+        hipSetDevice(dev);
+        for (int r = 0; r < kMaxLocalRanks; ++r)
+            if (ready[r]) hipEventDestroy(ready[r]);
+        if (done) hipEventDestroy(done);
+    }
+};
+
 namespace {
+// The R ranks of a local group meet: `mine` runs under the lock on arrival, `last` on the last arrival
+// (before anyone is released).  false: a peer never arrived within 60 s (the group is then broken).
+template <class Mine, class Last>
+bool lg_meet(ksched_lgroup *g, Mine mine, Last last) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (g->broken) return false;
+    const uint64_t gen = g->gen;
+    mine();
+    if (++g->arrived == g->R) {
+        last();
+        g->arrived = 0;
+        ++g->gen;
+        g->cv.notify_all();
+        return true;
+    }
+    if (!g->cv.wait_for(lk, std::chrono::seconds(60), [&] { return g->gen != gen; })) {
+        g->broken = true;
+        return false;
+    }
+    return true;
+}
+
 // all R ranks meet; returns the minimum of their values (false: a rank never arrived)
 bool group_min(ksched_group *g, int v, int *out) {
     std::unique_lock<std::mutex> lk(g->mu);
@@ -132,6 +184,7 @@ struct ksched_ctx {
     bool xchg_run = false;         // the current run uses the exchange
     uint32_t xchg_epoch = 1;       // granule tag base of the next call (identical on every rank)
     int32_t *d_xmin = nullptr;     // k_xchg_min result
+    std::shared_ptr<ksched_lgroup> lg;  // ranks of this process on this device (ksched_xchg_join_local)
     // diagnostics, read from the environment once at ksched_create (never a tuning switch):
     //   KSCHED_PERSIST_TRACE=1   per-batch phase stamps of the persistent pipeline, summary to stderr at sync
     //   KSCHED_COMMIT_STAMPS=1   commit phase cycle sums;  KSCHED_MERGE_STAMPS=1  merge phase cycle sums
@@ -280,6 +333,13 @@ int decide_fast53(ksched_ctx *c) {
     if (c->group) {
         int mn = flag;
         if (!group_min(c->group, flag, &mn)) return fail(c, KSCHED_E_DEVICE, "rank group: a peer never called run");
+        flag = mn;
+    } else if (c->xchg_run && c->lg) {
+        ksched_lgroup *g = c->lg.get();
+        int mn = flag;
+        if (!lg_meet(g, [&] { g->acc = g->arrived == 0 ? flag : std::min(g->acc, flag); }, [&] { g->result = g->acc; }))
+            return fail(c, KSCHED_E_DEVICE, "local rank group: a peer never called run");
+        mn = g->result;
         flag = mn;
     } else if (c->xchg_run) {
         // the ranks meet on the device through their rings (no collective launch)
@@ -513,6 +573,13 @@ int enqueue_batched(ksched_ctx *c) {
 void print_persist_trace(ksched_ctx *c) {
     std::vector<uint64_t> t((size_t)c->trace_cap * kTraceCols);
     if (hipMemcpy(t.data(), c->d_trace, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    // KSCHED_TRACE_DUMP=<path>: the raw stamps ([trace_cap][kTraceCols] u64, 100 MHz) for offline percentiles
+    if (const char *dump = std::getenv("KSCHED_TRACE_DUMP")) {
+        if (FILE *f = std::fopen(dump, "wb")) {
+            std::fwrite(t.data(), 8, t.size(), f);
+            std::fclose(f);
+        }
+    }
     auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
     double sum[16] = {};
     double scr[5] = {};  // WG 0 wave 0, screened batches: pass 1, bound merge, pass 2, exact phase (sums), exact rows
@@ -603,32 +670,37 @@ int enqueue_persistent(ksched_ctx *c) {
     // one workgroup per CU: the commit + G score workgroups.  At least ~96 rows per workgroup: a smaller
     // grid costs scan time but every list fewer shortens the merge (one rank's share of an 8-GPU c4,
     // 12.5k nodes: G = 128 -> 22.8 us per batch, 240 -> 23.8, 64 -> 24.6; round 2)
-    // A launch's workgroups are dealt round-robin to the 8 XCDs (32 CUs each) and never move to another
-    // XCD: kernels of ranks that share one device each take a multiple of 8 workgroups, so no XCD is
-    // asked for more CUs than it has (82 + 82 + 82 workgroups put 33 on two XCDs: one never started)
-    const int wgs = c->o.pipe_wgs > 0 ? std::min(c->o.pipe_wgs >= kXcds ? c->o.pipe_wgs / kXcds * kXcds : c->o.pipe_wgs,
-                                                 c->cus)
-                                      : c->cus;
+    // Ranks of a local group share the device in ONE cooperative launch: each takes an equal share of the
+    // CUs (one workgroup per CU: k_pipe's LDS admits one, checked against the occupancy query below), whole
+    // XCDs' worth (multiples of 8), one CU per XCD left over as a margin
+    const ksched_lgroup *lgp = c->xchg_run ? c->lg.get() : nullptr;
+    const int share = lgp ? (c->cus - kXcds) / lgp->R / kXcds * kXcds : c->cus;
+    const int wgs = std::min(share, c->o.pipe_wgs > 0 ? c->o.pipe_wgs : c->cus);
     // merger workgroups: kPipeMergeSlots pods each, one slot per pod of a batch
     const int M = (B + kPipeMergeSlots - 1) / kPipeMergeSlots;
     const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1 - M, (int64_t)kPipeMergeThreads,
                                                                (n_geom + 95) / 96}));
     if (wgs < 2 + M) return 1;
     const int R = (int)((n_geom + G - 1) / G);
-    PersistArgs a{};
+    PipeLaunch L{};
+    PersistArgs &a = L.P[0];
     a.rows_per_wg = R;
     a.G = G;
     a.M = M;
     a.B = B;
+    L.R = 1;
+    L.base[1] = 1 + G + M;
     PipeInfo info{};
     const bool f53 = c->fast53, lab = c->o.use_labels != 0;
-    hipError_t e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, a, 0, &info, c->stream);
+    hipError_t e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, L, 0, &info, c->stream);
     if (e == hipErrorNotSupported) return 1;
     HIPCHK(c, e);
     if (c->diag.debug)
-        fprintf(stderr, "[ksched pipe] G=%d rows/wg=%d LDS %zu+%zu B, %d VGPRs, %zu B scratch\n", G, R, info.lds,
-                info.static_lds, info.vgprs, info.spill);
+        fprintf(stderr, "[ksched pipe] G=%d rows/wg=%d LDS %zu+%zu B, %d VGPRs, %zu B scratch, %d WG/CU\n", G, R,
+                info.lds, info.static_lds, info.vgprs, info.spill, info.occ);
     if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
+    if (lgp && (info.occ < 1 || (int64_t)lgp->R * (1 + G + M) > (int64_t)(c->cus - kXcds) * info.occ))
+        return fail(c, KSCHED_E_INVALID, "local rank group: the ranks' grids do not fit the device together");
     // workspace: part lists [kPipeLag][B][G][KC] + counts [kPipeLag][B][G] (score(b + kPipeLag) reuses
     // batch b's), list ring 4 x (B*K Rec + B fc), XBuf ring
     const size_t part_b = align_up((size_t)kPipeLag * B * G * KC * sizeof(Cand), 256);
@@ -699,10 +771,45 @@ int enqueue_persistent(ksched_ctx *c) {
     int e0 = -1;
     HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, sS));
     // cooperative launch: the runtime checks the grid against the occupancy query, so every workgroup is
-    // resident at once.  Ranks sharing one device (pipe_wgs) launch plainly: each takes a share of the CUs
-    // and the cooperative launch would serialise them.
-    const int how = c->o.pipe_wgs > 0 ? 2 : 1;
-    e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, a, how, nullptr, sS);
+    // resident at once.  A local group's ranks stage their arguments and the last to arrive launches all
+    // of them as one grid on its stream, behind every rank's pre-launch work; the others' streams wait for it.
+    if (lgp) {
+        ksched_lgroup *g = c->lg.get();
+        const int me = c->o.rank;
+        HIPCHK(c, hipEventRecord(g->ready[me], sS));
+        const bool met = lg_meet(
+            g,
+            [&] {
+                g->L.P[me] = a;
+                g->stream[me] = sS;
+                if (g->arrived == 0) {
+                    g->kc = KC; g->k = K; g->prio = c->o.priority; g->dom = c->o.domain; g->lab = lab; g->f53 = f53;
+                    g->launch_err = hipSuccess;
+                } else if (g->kc != KC || g->k != K || g->prio != c->o.priority || g->dom != c->o.domain ||
+                           g->lab != lab || g->f53 != f53) {
+                    g->launch_err = hipErrorInvalidValue;  // the ranks disagree on the kernel
+                }
+            },
+            [&] {
+                if (g->launch_err != hipSuccess) return;
+                g->L.R = g->R;
+                g->L.base[0] = 0;
+                for (int r = 0; r < g->R; ++r) g->L.base[r + 1] = g->L.base[r] + 1 + g->L.P[r].G + g->L.P[r].M;
+                hipError_t le = hipSuccess;
+                for (int r = 0; r < g->R && le == hipSuccess; ++r)
+                    if (r != me) le = hipStreamWaitEvent(sS, g->ready[r], 0);
+                if (le == hipSuccess) le = launch_pipe(g->kc, g->k, g->prio, g->dom, g->lab, g->f53, g->L, 1, nullptr, sS);
+                if (le == hipSuccess) le = hipEventRecord(g->done, sS);
+                g->launch_err = le;
+            });
+        if (!met) return fail(c, KSCHED_E_DEVICE, "local rank group: a peer never launched");
+        if (g->launch_err != hipSuccess)
+            return fail(c, KSCHED_E_DEVICE, std::string("local rank group launch: ") + hipGetErrorString(g->launch_err));
+        HIPCHK(c, hipStreamWaitEvent(sS, g->done, 0));  // (a no-op on the launching rank's own stream)
+        e = hipSuccess;
+    } else {
+        e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, L, 1, nullptr, sS);
+    }
     if (e == hipErrorCooperativeLaunchTooLarge && !c->xchg_run) {  // the stream pipeline runs instead
         if (c->diag.debug) fprintf(stderr, "[ksched pipe] cooperative launch too large: stream pipeline\n");
         (void)hipGetLastError();
@@ -859,8 +966,9 @@ int ksched_destroy(ksched_ctx *c) {
     for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
     hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_xmin);
-    for (int r = 0; r < kMaxXchgRanks; ++r)
-        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx) hipIpcCloseMemHandle(c->rx_peer[r]);
+    for (int r = 0; r < kMaxXchgRanks; ++r)  // a local group's peers are its own contexts' rings, not IPC maps
+        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[r]);
+    c->lg.reset();
     hipFree(c->d_rx);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
@@ -933,6 +1041,7 @@ int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) 
     if (R < 2 || R > kMaxXchgRanks) return fail(c, KSCHED_E_INVALID, "xchg_export: 2 <= nranks <= 8");
     if (c->B > 64) return fail(c, KSCHED_E_INVALID, "xchg_export: the persistent pipeline needs batch <= 64");
     if (c->group) return fail(c, KSCHED_E_STATE, "xchg_export: context uses an in-process rank group");
+    if (c->lg) return fail(c, KSCHED_E_STATE, "xchg_export: context is in a local rank group (xchg_join_local)");
     HIPCHK(c, hipSetDevice(c->dev));
     const size_t bytes = xchg_ring_bytes(R, c->B, c->K);
     if (!c->d_rx) {
@@ -955,9 +1064,10 @@ int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
     HIPCHK(c, hipSetDevice(c->dev));
     const int R = c->o.nranks;
     for (int r = 0; r < kMaxXchgRanks; ++r) {
-        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx) hipIpcCloseMemHandle(c->rx_peer[r]);
+        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[r]);
         c->rx_peer[r] = nullptr;
     }
+    c->lg.reset();
     c->xchg_ready = false;
     for (int r = 0; r < R; ++r) {
         if (r == c->o.rank) { c->rx_peer[r] = static_cast<char *>(c->d_rx); continue; }
@@ -973,6 +1083,50 @@ int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
 }
 
 int ksched_xchg_ready(const ksched_ctx *c) { return c && c->xchg_ready ? 1 : 0; }
+
+int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) {
+    if (!ctxs || n < 2 || n > kMaxLocalRanks) return KSCHED_E_INVALID;
+    for (int r = 0; r < n; ++r)
+        if (!ctxs[r]) return KSCHED_E_INVALID;
+    ksched_ctx *c0 = ctxs[0];
+    for (int r = 0; r < n; ++r) {
+        ksched_ctx *c = ctxs[r];
+        if (c->o.nranks != n || c->o.rank != r)
+            return fail(c, KSCHED_E_INVALID, "xchg_join_local: ctxs[r] must be rank r of nranks = n");
+        if (c->dev != c0->dev) return fail(c, KSCHED_E_INVALID, "xchg_join_local: the ranks must share one device");
+        if (c->B > 64) return fail(c, KSCHED_E_INVALID, "xchg_join_local: the persistent pipeline needs batch <= 64");
+        if (c->group) return fail(c, KSCHED_E_STATE, "xchg_join_local: context uses an in-process rank group");
+        if (c->B != c0->B || c->K != c0->K || c->KC != c0->KC || c->o.priority != c0->o.priority ||
+            c->o.domain != c0->o.domain || c->o.use_labels != c0->o.use_labels)
+            return fail(c, KSCHED_E_INVALID, "xchg_join_local: the ranks' options differ");
+    }
+    auto g = std::make_shared<ksched_lgroup>();
+    g->R = n;
+    g->dev = c0->dev;
+    HIPCHK(c0, hipSetDevice(c0->dev));
+    for (int r = 0; r < n; ++r) HIPCHK(c0, hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming));
+    HIPCHK(c0, hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
+    const size_t bytes = xchg_ring_bytes(n, c0->B, c0->K);
+    for (int r = 0; r < n; ++r) {
+        ksched_ctx *c = ctxs[r];
+        if (!c->d_rx) {  // the same ring as xchg_export's (uncached), never IPC-exported
+            HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
+            HIPCHK(c, hipMemset(c->d_rx, 0, bytes));
+            c->rx_bytes = bytes;
+        }
+    }
+    for (int r = 0; r < n; ++r) {
+        ksched_ctx *c = ctxs[r];
+        for (int q = 0; q < kMaxXchgRanks; ++q) {
+            if (c->rx_peer[q] && c->rx_peer[q] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[q]);
+            c->rx_peer[q] = q < n ? static_cast<char *>(ctxs[q]->d_rx) : nullptr;
+        }
+        c->lg = g;
+        c->xchg_ready = true;
+        c->xchg_epoch = 1;
+    }
+    return KSCHED_OK;
+}
 
 int ksched_xchg_close(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
@@ -1441,7 +1595,8 @@ static int sync_impl(ksched_ctx *c) {
     }
     if (e >= 5 && e <= 11) {
         hipMemset(c->d_err, 0, sizeof(int32_t));
-        static const char *what[] = {"the commit's wait for the merges", "a score workgroup's wait for commit(b-2)",
+        static const std::string lagw = "a score or merger workgroup's wait for commit(b-" + std::to_string(kPipeLag) + ")";
+        static const char *what[] = {"the commit's wait for the merges", lagw.c_str(),
                                      "a merger's wait for the score workgroups", "the score grid's plan (idle)",
                                      "the commit's plan (idle)",
                                      "a merger's wait for a peer rank's candidate lists (node-sharded exchange)",

@@ -468,17 +468,28 @@ struct PipeInfo {
     size_t static_lds;
     int vgprs;
     size_t spill;       // private (scratch) bytes per thread
+    int occ;            // workgroups per CU the occupancy query admits at that LDS (1: one per CU)
 };
-// launch: 0 = query PipeInfo only, 1 = cooperative launch (the runtime checks the grid against the
-// occupancy query), 2 = plain launch (ranks sharing one device, each with a fraction of the CUs).
+// One launch of k_pipe: the grids of R ranks (R = 1: a single rank) back to back, rank r's workgroups
+// [base[r], base[r + 1]).  R > 1 only for ranks of ONE process sharing ONE device (ksched_xchg_join_local):
+// their persistent kernels must be resident at once, which one cooperative launch guarantees and separate
+// launches do not.
+constexpr int kMaxLocalRanks = 4;
+struct PipeLaunch {
+    PersistArgs P[kMaxLocalRanks];
+    int32_t R;
+    int32_t base[kMaxLocalRanks + 1];
+};
+// launch: 0 = query PipeInfo only (L.P[0]), 1 = cooperative launch (the runtime checks the grid against the
+// occupancy query, so every workgroup of every rank in L is resident at once).
 // hipErrorNotSupported: no instantiation for (KC, K) -- the caller runs the stream pipeline.
-hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PipeLaunch &L, int launch, PipeInfo *info,
                            hipStream_t s);
-hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PipeLaunch &L, int launch, PipeInfo *info,
                              hipStream_t s);
-hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PipeLaunch &L, int launch, PipeInfo *info,
                               hipStream_t s);
-inline hipError_t launch_pipe(int KC, int K, int prio, int dom, bool lab, bool f53, const PersistArgs &a, int launch,
+inline hipError_t launch_pipe(int KC, int K, int prio, int dom, bool lab, bool f53, const PipeLaunch &a, int launch,
                               PipeInfo *info, hipStream_t s) {
     if (prio == kPrioPrice) return pipe_part_price(KC, K, lab, false, a, launch, info, s);
     if (dom == kDomFeasible) return pipe_part_res_feas(KC, K, lab, f53, a, launch, info, s);

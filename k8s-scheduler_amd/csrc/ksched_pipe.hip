@@ -21,7 +21,7 @@
 // MI355X_MICROARCH "valid forms" row 1 (sc1 stores, every storing wave drained, one lane's counter
 // update; sc1 loads after the poll) and every wait is bounded (PersistArgs::timeout_ticks -> error words
 // 5..11).  Snapshot semantics (lag kPipeLag = 3): score(b) sees every commit up to b - 3, commit(b)
-// inherits the nodes b - 2 and b - 1 committed (oracle/cpu_ref.c or_schedule_pipelined, lag 3).
+// inherits the nodes b - 2 and b - 1 committed (oracle/cpu_ref.c or_schedule_lagged at lag 3).
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 
@@ -62,7 +62,7 @@ __device__ __forceinline__ void role_sync(unsigned *ctr, unsigned &target, unsig
 struct alignas(16) PipeCtl {
     unsigned sbar, mbar;          // role barrier counters
     int32_t s_stop, m_stop;
-    int64_t s_p0, s_done;         // score role: this batch's plan and the cursor after commit(b-2)
+    int64_t s_p0, s_done;         // score role: this batch's plan and the cursor after commit(b - kPipeLag)
     int64_t m_p0, m_done;         // merge role: the same, read by its own poll
     int32_t c_stop;               // commit workgroup
     int32_t s_ex;                 // score role: rows of this batch scored exactly (screened scan)
@@ -350,7 +350,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             if (b >= kPipeLag && !stop) {
-                nxv = (int)(uint32_t)ld_coh(&xb->count);  // one address: one request for the wave
+                // {count, batch tag} in one granule: an idle commit (plan -1) leaves its ring slot untouched,
+                // so a slot still tagged with an older batch is an empty export (never a torn one)
+                const uint64_t hdr = ld_coh(&xb->count);  // one address: one request for the wave
+                nxv = (uint32_t)(hdr >> 32) == (uint32_t)(b - kPipeLag) ? (int)(uint32_t)hdr : 0;
                 if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
                     const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[lane]);
                     w0 = ld_coh(w); w4 = ld_coh(w + 4); w5 = ld_coh(w + 5); w6 = ld_coh(w + 6);
@@ -885,7 +888,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
 }
 
 // ------------------------------------------------------------------------------------------------
-// COMMIT role (workgroup 0, all 16 waves): batch after batch, wait for the B merges of an active batch
+// COMMIT role (workgroup 0, all kPipeWaves = 12 waves): batch after batch, wait for the B merges of an active batch
 // (Ctl::merged), commit it (commit_spc_batch: lists read with sc1 loads; export, plans and cursor left as
 // sc1 stores), publish Ctl::committed.  Once every pod is resolved it publishes a committed count no wait
 // can exceed, so every workgroup still waiting sees the end.
@@ -994,26 +997,32 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
 // The kernel.  <= 128 VGPRs (1024 threads: four waves per SIMD).
 // ------------------------------------------------------------------------------------------------
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
-__global__ __launch_bounds__(kPipeThreads) void k_pipe(PersistArgs P) {
+__global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (blockIdx.x == 0) {
+    // this workgroup's rank (ranks of one process sharing the device run as one launch; R = 1 otherwise)
+    int r = 0;
+#pragma unroll
+    for (int i = 1; i < kMaxLocalRanks; ++i) r += (i < L.R && (int)blockIdx.x >= L.base[i]) ? 1 : 0;
+    const PersistArgs &P = L.P[r];
+    const int blk = (int)blockIdx.x - L.base[r];
+    if (blk == 0) {
 #ifndef KSCHED_PROBE_NO_COMMIT
         commit_role<K, PRIO, DOM, LAB, F53>(P, smem);
 #endif
         return;
     }
-    if ((int)blockIdx.x <= P.G) {
+    if (blk <= P.G) {
         PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
         if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
         __syncthreads();
 #ifndef KSCHED_PROBE_NO_SCORE
-        score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, (int)blockIdx.x - 1);
+        score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, blk - 1);
 #endif
         return;
     }
     // a merger workgroup: kMS independent pod slots of kMT threads
     const int slot = (int)threadIdx.x / kMT;
-    const int id = ((int)blockIdx.x - 1 - P.G) * kMS + slot;
+    const int id = (blk - 1 - P.G) * kMS + slot;
     char *sbase = smem + (size_t)slot * MergeLayout<KC, K>::slot_bytes;
     if (threadIdx.x % kMT == 0) reinterpret_cast<MergeCtl *>(sbase)->mbar = 0;
     __syncthreads();  // the only workgroup-wide barrier: before the slots part
@@ -1023,17 +1032,19 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PersistArgs P) {
 }
 
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
-hipError_t pipe_one(const PersistArgs &a0, int launch, PipeInfo *info, hipStream_t s) {
+hipError_t pipe_one(const PipeLaunch &L0, int launch, PipeInfo *info, hipStream_t s) {
     auto fn = k_pipe<KC, K, PRIO, DOM, LAB, F53>;
-    PersistArgs a = a0;
+    PipeLaunch L = L0;
     // the screened scan when its reciprocals fit beside everything else, keeping pass 1's per-pair records
-    // when those fit too
+    // when those fit too (every rank of a launch has the same geometry up to one row)
     constexpr size_t kLds = (size_t)160 * 1024;
-    const int R = a.rows_per_wg;
-    a.screen_h = ScoreLayout<KC, K>::total_with_hrec(R) <= kLds ? 1 : 0;
-    a.screen_ok = ScoreLayout<KC, K>::total_screen(R) <= kLds ? 1 : 0;
-    const size_t sl = a.screen_h ? ScoreLayout<KC, K>::total_with_hrec(R)
-                                 : (a.screen_ok ? ScoreLayout<KC, K>::total_screen(R) : ScoreLayout<KC, K>::total(R));
+    int R = 0;
+    for (int r = 0; r < L.R; ++r) R = L.P[r].rows_per_wg > R ? L.P[r].rows_per_wg : R;
+    const int sh = ScoreLayout<KC, K>::total_with_hrec(R) <= kLds ? 1 : 0;
+    const int so = ScoreLayout<KC, K>::total_screen(R) <= kLds ? 1 : 0;
+    for (int r = 0; r < L.R; ++r) { L.P[r].screen_h = sh; L.P[r].screen_ok = so; }
+    const size_t sl = sh ? ScoreLayout<KC, K>::total_with_hrec(R)
+                         : (so ? ScoreLayout<KC, K>::total_screen(R) : ScoreLayout<KC, K>::total(R));
     const size_t cl = commit_total_bytes<K>(), ml = MergeLayout<KC, K>::total;
     const size_t lds = sl > cl ? (sl > ml ? sl : ml) : (cl > ml ? cl : ml);
     if (info) {
@@ -1044,21 +1055,28 @@ hipError_t pipe_one(const PersistArgs &a0, int launch, PipeInfo *info, hipStream
         info->static_lds = at.sharedSizeBytes;
         info->vgprs = at.numRegs;
         info->spill = at.localSizeBytes;
+        info->occ = 0;
+        if (lds + at.sharedSizeBytes <= kLds) {
+            e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&info->occ, fn, kPipeThreads, lds);
+            if (e != hipSuccess) return e;
+        }
     }
     if (!launch) return hipSuccess;
-    if (a.G > kMT || a.B > 64 || a.M * kMS < a.B) return hipErrorInvalidValue;
+    if (L.R < 1 || L.R > kMaxLocalRanks || L.base[0] != 0) return hipErrorInvalidValue;
+    for (int r = 0; r < L.R; ++r) {
+        const PersistArgs &a = L.P[r];
+        if (a.G > kMT || a.B > 64 || a.M * kMS < a.B || L.base[r + 1] - L.base[r] != 1 + a.G + a.M)
+            return hipErrorInvalidValue;
+    }
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    if (launch == 1) {
-        void *args[] = {const_cast<PersistArgs *>(&a)};
-        return hipLaunchCooperativeKernel((const void *)fn, dim3(1 + a.G + a.M), dim3(kPipeThreads), args, (unsigned)lds, s);
-    }
-    hipLaunchKernelGGL(fn, dim3(1 + a.G + a.M), dim3(kPipeThreads), lds, s, a);
-    return hipGetLastError();
+    void *args[] = {&L};
+    return hipLaunchCooperativeKernel((const void *)fn, dim3(L.base[L.R]), dim3(kPipeThreads), args, (unsigned)lds, s);
 }
 
 template <int PRIO, int DOM, bool LAB, bool F53>
-hipError_t pipe_kk(int KC, int K, const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+hipError_t pipe_kk(int KC, int K, const PipeLaunch &a, int launch, PipeInfo *info, hipStream_t s) {
     if (KC == 4 && K == 4) return pipe_one<4, 4, PRIO, DOM, LAB, F53>(a, launch, info, s);
     if (KC == 4 && K == 8) return pipe_one<4, 8, PRIO, DOM, LAB, F53>(a, launch, info, s);
     if (KC == 4 && K == 16) return pipe_one<4, 16, PRIO, DOM, LAB, F53>(a, launch, info, s);
@@ -1068,7 +1086,7 @@ hipError_t pipe_kk(int KC, int K, const PersistArgs &a, int launch, PipeInfo *in
 }
 
 template <int PRIO, int DOM>
-hipError_t pipe_lf(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info, hipStream_t s) {
+hipError_t pipe_lf(int KC, int K, bool lab, bool f53, const PipeLaunch &a, int launch, PipeInfo *info, hipStream_t s) {
     if (PRIO == kPrioPrice) f53 = false;  // best-price never divides
     if (lab) return f53 ? pipe_kk<PRIO, DOM, true, true>(KC, K, a, launch, info, s)
                         : pipe_kk<PRIO, DOM, true, false>(KC, K, a, launch, info, s);
@@ -1079,7 +1097,7 @@ hipError_t pipe_lf(int KC, int K, bool lab, bool f53, const PersistArgs &a, int 
 }  // namespace
 
 #if KSCHED_PIPE_PART == 0
-hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_price(int KC, int K, bool lab, bool f53, const PipeLaunch &a, int launch, PipeInfo *info,
                            hipStream_t s) {
     return pipe_lf<kPrioPrice, kDomFeasible>(KC, K, lab, f53, a, launch, info, s);
 }
@@ -1112,12 +1130,12 @@ hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hip
     return hipGetLastError();
 }
 #elif KSCHED_PIPE_PART == 1
-hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_res_all(int KC, int K, bool lab, bool f53, const PipeLaunch &a, int launch, PipeInfo *info,
                              hipStream_t s) {
     return pipe_lf<kPrioResource, kDomAll>(KC, K, lab, f53, a, launch, info, s);
 }
 #else
-hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PersistArgs &a, int launch, PipeInfo *info,
+hipError_t pipe_part_res_feas(int KC, int K, bool lab, bool f53, const PipeLaunch &a, int launch, PipeInfo *info,
                               hipStream_t s) {
     return pipe_lf<kPrioResource, kDomFeasible>(KC, K, lab, f53, a, launch, info, s);
 }

@@ -23,7 +23,7 @@ E_UNKNOWN_NODE = -6
 NO_FIT = -1
 NO_POSITIVE_SCORE = -2
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MODE_EXACT, MODE_BATCHED, MODE_AUTO = 0, 1, 2
 PIPELINE_AUTO, PIPELINE_STREAM = 0, 1
 PRIORITY_RESOURCE, PRIORITY_BEST_PRICE = 0, 1
@@ -88,6 +88,7 @@ SIGNATURES = [
     ("ksched_xchg_import", C.c_int, [CTX, C.c_char_p]),
     ("ksched_xchg_ready", C.c_int, [CTX]),
     ("ksched_xchg_close", C.c_int, [CTX]),
+    ("ksched_xchg_join_local", C.c_int, [C.POINTER(CTX), C.c_int32]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
     ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),

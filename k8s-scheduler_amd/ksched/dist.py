@@ -108,3 +108,16 @@ def gather_node_state(local_state, world: int):
         dist.all_gather_object(parts, t.numpy())
         out.append(np.concatenate(parts))
     return tuple(out)
+
+
+def make_local_xchg_group(cl, world: int, device: int = 0, **kw):
+    """`world` node-sharded ranks of cluster `cl` as contexts of THIS process on ONE device, joined by the
+    device-side exchange without IPC (ksched_xchg_join_local): their persistent kernels run as one
+    cooperative launch, so all ranks' grids are resident at once.  The caller runs each rank's schedule
+    calls in its own thread.  Returns [(engine, (lo, hi)) per rank]."""
+    from . import _lib as L
+    from .engine import Engine
+    out = [make_sharded_engine(cl, r, world, device=device, mode=L.MODE_BATCHED, comm=False, **kw)
+           for r in range(world)]
+    Engine.xchg_join_local([e for e, _ in out])
+    return out

@@ -117,6 +117,13 @@ class Engine:
         """Turn the device exchange off on this rank (the ranks must agree on the transport)."""
         self._chk(L.lib().ksched_xchg_close(self._ctx), "xchg_close")
 
+    @staticmethod
+    def xchg_join_local(engines):
+        """Ranks as threads of this process on one device (engines[r] = rank r): the device exchange without
+        IPC, the ranks' persistent kernels as ONE cooperative launch (ksched_xchg_join_local)."""
+        arr = (L.CTX * len(engines))(*[e._ctx for e in engines])
+        L.check(L.lib().ksched_xchg_join_local(arr, len(engines)), engines[0]._ctx, "xchg_join_local")
+
     @property
     def xchg_ready(self) -> bool:
         return bool(L.lib().ksched_xchg_ready(self._ctx))

@@ -17,16 +17,19 @@ DRIVER = os.path.join(ROOT, "integration", "ksched_driver")
 BIND_FAILED = -3
 
 
-def write_input(path, cl, fails):
+def write_input(path, cl, fails, events=()):
+    """events: the bound-pod watch's (type 1 ADDED | 2 DELETED, node index or -1, cpu, mem, ours)"""
     n, p = cl.n_nodes, cl.n_pods
     lab = cl.labels if cl.labels is not None else np.zeros(n, np.uint64)
     pr = cl.price if cl.price is not None else np.zeros(n, np.float32)
     sel = cl.selector if cl.selector is not None else np.zeros(p, np.uint64)
-    hdr = np.array([n, p, len(fails), cl.priority, cl.domain, int(cl.use_labels), int(cl.price is not None)], np.int64)
+    hdr = np.array([n, p, len(fails), cl.priority, cl.domain, int(cl.use_labels), int(cl.price is not None),
+                    len(events)], np.int64)
+    ev = np.asarray(events, np.int64).reshape(-1, 5)
     with open(path, "wb") as f:
         for a, t in ((hdr, np.int64), (cl.alloc_cpu, np.int64), (cl.alloc_mem, np.int64), (cl.alloc_pods, np.int64),
                      (lab, np.uint64), (pr, np.float32), (cl.req_cpu, np.int64), (cl.req_mem, np.int64),
-                     (cl.req_pods, np.int64), (sel, np.uint64), (np.asarray(fails, np.int64), np.int64)):
+                     (cl.req_pods, np.int64), (sel, np.uint64), (np.asarray(fails, np.int64), np.int64), (ev, np.int64)):
             f.write(np.ascontiguousarray(a, dtype=t).tobytes())
 
 
@@ -100,3 +103,35 @@ def test_driver_call_sequence(gpu_available, oracle_mod, tmp_path, case):
         assert np.array_equal(counts, wc), f"mode {mode}: FailedScheduling counts differ"
         assert all(np.array_equal(a, b) for a, b in zip(final, wst)), f"mode {mode}: final state differs"
         assert stats[2] == (wi == BIND_FAILED).sum() and stats[2] <= stats[0] <= 1 + stats[2]
+
+
+def test_driver_watch_events(gpu_available, oracle_mod, tmp_path):
+    """The shim's onPodEvent path: after a pass, pods bound / deleted by others move the device state by their
+    requests (one pod each), the ADDED echo of this run's own binds is skipped, and an event on a node missing
+    from the node list ends the driver with KSCHED_E_UNKNOWN_NODE (the reference's usedResource panics there,
+    anchor/predicate.go:94-99)."""
+    from ksched import cluster
+    cl = cluster.make_cluster("c3", n_nodes=1500, n_pods=800)
+    wi, _, _, _, wst = expected(cl, [], oracle_mod)
+    j0 = int(wi[wi >= 0][0])
+    events = [(1, 7, 900, 1 << 20, 0),   # another scheduler bound a pod on node 7
+              (2, 11, 250, 4096, 0),     # a bound pod on node 11 was deleted
+              (1, j0, 12345, 6789, 1),   # the echo of this run's first bind: skipped
+              (1, 7, 100, 2048, 0)]
+    write_input(tmp_path / "in.bin", cl, [], events)
+    r = subprocess.run([DRIVER, str(tmp_path / "in.bin"), str(tmp_path / "out.bin"), "1", "16", "64"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    _, idx, _, _, _, final = read_output(tmp_path / "out.bin", cl.n_nodes, cl.n_pods)
+    assert np.array_equal(idx, wi)
+    want = [a.copy() for a in wst]
+    for t, j, c, m, ours in events:
+        if t == 1 and ours:
+            continue
+        s = -1 if t == 1 else 1
+        want[0][j] += s * c; want[1][j] += s * m; want[2][j] += s
+    assert all(np.array_equal(a, b) for a, b in zip(final, want)), "watch deltas differ"
+    write_input(tmp_path / "in2.bin", cl, [], events + [(1, -1, 100, 100, 0)])
+    r = subprocess.run([DRIVER, str(tmp_path / "in2.bin"), str(tmp_path / "out2.bin"), "1", "16", "64"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 6 and "unknown node" in r.stderr, (r.returncode, r.stderr)

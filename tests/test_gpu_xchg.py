@@ -1,65 +1,68 @@
-"""Node-sharded persistent pipeline with the device-side exchange (ksched_xchg_*), R processes on the
-one GPU of the test box: every rank's results must equal the CPU oracle's sequential schedule, bit for
-bit, and the ranks' node shards together must equal the oracle's final state.  Exercises the product
-multi-rank code: global node indices at node_offset > 0, granule exchange through IPC-mapped rings,
-the rank merge in the merger workgroups and the owner-only write-back (the xGMI transport itself needs
-several GPUs)."""
-import multiprocessing as mp
-import os
-import socket
-import sys
+"""Node-sharded persistent pipeline with the device-side exchange, R ranks on the one GPU of the test box:
+every rank's results must equal the CPU oracle's sequential schedule, bit for bit, and the ranks' node
+shards together must equal the oracle's final state.  Exercises the product multi-rank code: global node
+indices at node_offset > 0, granule exchange through the ranks' receive rings, the rank merge in the merger
+workgroups and the owner-only write-back (the xGMI transport itself needs several GPUs).
+
+The ranks are threads of this process joined by ksched_xchg_join_local: their kernels run as ONE cooperative
+launch, so every rank's grid is resident at once by construction.  (Round 3 ran them as separate processes
+with separate plain launches; one rank's kernel was once descheduled for the whole 10 s timeout -- nothing
+makes the launches of different processes co-resident.)"""
+import threading
 
 import numpy as np
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd"), os.path.join(ROOT, "oracle"), os.path.dirname(__file__)]
+pytestmark = pytest.mark.gpu
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def run_local(cl, world, calls=2):
+    from ksched.dist import make_local_xchg_group
+    ranks = make_local_xchg_group(cl, world, device=0, topk=16, batch=64)
+    for e, _ in ranks:
+        assert e.xchg_ready, "exchange join failed"
+        e.save_state()
+    out = [None] * world
+    errs = []
+
+    def work(r):
+        try:
+            e = ranks[r][0]
+            res = []
+            for _ in range(calls):  # repeated calls: the granule tags advance across calls
+                e.restore_state()
+                oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+                st = e.stats()
+                res.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"]))
+            out[r] = (res, e.read_nodes())
+        except Exception as ex:  # surfaced below
+            errs.append((r, repr(ex)))
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=150)
+    for e, _ in ranks:
+        e.close()
+    assert not errs, errs
+    assert all(o is not None for o in out), "a rank did not finish"
+    return out
 
 
-@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,nn,pp,world", [("c3", 24000, 3000, 2), ("c5hc", 20000, 3000, 2), ("c4", 30000, 2500, 3),
-                                                     ("c4", 100000, 2500, 2)])
-def test_xchg_ranks_match_oracle(cfg, nn, pp, world):
-    import oracle as O
-    import xchg_worker
+                                             ("c4", 100000, 2500, 2), ("c5", 40000, 2000, 4)])
+def test_xchg_ranks_match_oracle(gpu_available, oracle_mod, cfg, nn, pp, world):
     from ksched import cluster
     cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
-    want = O.schedule(cl, nthreads=8)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _port()
-    procs = [ctx.Process(target=xchg_worker.run_rank, args=(r, world, port, cfg, nn, pp, 2, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    res, errs = {}, {}
-    try:
-        for _ in range(world):
-            r, status, out, rng, state = q.get(timeout=110)
-            if status == "ok":
-                res[r] = (out, rng, state)
-            else:
-                errs[r] = out
-    finally:
-        for p in procs:
-            p.join(timeout=15)
-            if p.is_alive():
-                p.kill()
-    assert not errs, "\n".join(f"rank {r}: {t}" for r, t in sorted(errs.items()))
+    want = oracle_mod.schedule(cl, nthreads=8)
+    out = run_local(cl, world)
     for r in range(world):
-        out, rng, state = res[r]
-        for oi, osb, of, pipe, nb, ntr in out:
+        for oi, osb, of, pipe, nb, ntr in out[r][0]:
             assert pipe == "persistent", f"rank {r} ran the {pipe} pipeline"
             assert np.array_equal(oi, want[0]), f"rank {r}: assignments differ at {np.nonzero(oi != want[0])[0][:5]}"
             assert np.array_equal(osb, want[1].view(np.int64)), f"rank {r}: score bits differ"
             assert np.array_equal(of, want[2]), f"rank {r}: feasible counts differ"
-    got = [np.concatenate([res[r][2][k] for r in range(world)]) for k in range(3)]
+    got = [np.concatenate([out[r][1][k] for r in range(world)]) for k in range(3)]
     for k in range(3):
         assert np.array_equal(got[k], want[3][k]), f"final node state (resource {k}) differs"
