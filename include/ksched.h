@@ -101,6 +101,11 @@ typedef struct ksched_stats {
     int64_t kernel_launches[4]; /* number of timed batches (launch groups) behind kernel_ms */
     int64_t kernel_pairs[4];    /* pod-node pairs evaluated by the timed family-0 launches */
     int64_t pipeline;           /* which device pipeline ran the last call: KSCHED_PIPE_* (ABI 2) */
+    int64_t rescues;            /* persistent pipeline (ABI 5): exhausted candidate lists resolved by a full scan
+                                   of the untouched nodes instead of truncating their batch */
+    int64_t exact_rows;         /* persistent pipeline: node rows scored exactly (f64) by the score workgroups,
+                                   summed over batches -- the screened scan's survivors plus unscreened batches */
+    int64_t scan_rows;          /* ... and node rows scanned (each row once per active batch) */
 } ksched_stats;
 
 enum {

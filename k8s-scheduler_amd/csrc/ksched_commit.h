@@ -140,6 +140,66 @@ __device__ __forceinline__ double lane_key(bool f, int64_t rc, int64_t rm, int64
     return el ? k : -__builtin_inf();
 }
 
+// What a rescue found: the best node outside the touched set (idx = kNoIdx: none eligible) and its state.
+struct RescueOut {
+    double key;
+    int32_t idx;
+    int64_t a[3];
+    uint64_t labels;
+    float price;
+};
+
+// The rescue of pod f's exhausted candidate list (wave 0 of the persistent commit; pod f's list is cut, every
+// entry is touched and no touched node beats its last entry, so the best untouched node may lie outside it):
+// publish the request -- pod f's request and the touched set T = ti[0, nT) -- as sc1 stores, drained, then the
+// request number in Ctl::rescue_req; the B merger slots each scan a share of the node rows (serve_rescue,
+// ksched_pipe.hip) and count their results in Ctl::rescue_done; lane = slot, the wave's arg-best is the answer.
+// false: the wait timed out (error 12).  Restated by oracle/cpu_ref.c or_rescue.
+__device__ __forceinline__ bool commit_rescue(const CommitArgs &A, int f, int64_t rc, int64_t rm, int64_t rp,
+                                              uint64_t sel, const int32_t *ti, int nT, RescueOut *o) {
+    const int lane = threadIdx.x & 63;
+    RescueReq *rq = reinterpret_cast<RescueReq *>(A.rescue);
+    for (int t = lane; t < nT; t += 64) st_coh(&rq->ti[t], (uint64_t)(int64_t)ti[t]);
+    if (lane == 0) {
+        st_coh(&rq->rc, (uint64_t)rc);
+        st_coh(&rq->rm, (uint64_t)rm);
+        st_coh(&rq->rp, (uint64_t)rp);
+        st_coh(&rq->sel, sel);
+        st_coh(&rq->nT, (uint64_t)nT);
+    }
+    drain_stores();  // every store of the request, before the request number
+    const unsigned long long q = (unsigned long long)A.loc->rseq + 1ull;
+    lds_order();
+    int ok = 1;
+    if (lane == 0) {
+        A.loc->rseq = (int64_t)q;
+        __hip_atomic_store(&A.ctl->rescue_req.v, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long seen = 0;
+        ok = poll_ge(&A.ctl->rescue_done.v, q * (unsigned long long)A.rescue_n, A.timeout_ticks, &A.ctl->polls_rmw,
+                     &seen) ? 1 : 0;
+        if (!ok) atomicCAS(A.err, 0, 12);
+    }
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    if (!ok) return false;
+    const Rec *res = reinterpret_cast<const Rec *>(A.rescue + kRescueResOff);
+    double k = -__builtin_inf();
+    int32_t ix = kNoIdx, src = lane;
+    uint64_t w[7] = {0, 0, 0, 0, 0, 0, 0};
+    if (lane < A.rescue_n) {
+        const uint64_t *rw = reinterpret_cast<const uint64_t *>(res + lane);
+#pragma unroll
+        for (int i = 0; i < 7; ++i) w[i] = ld_coh(rw + i);
+        if ((uint32_t)(w[1] >> 32) != 0) { k = __longlong_as_double((long long)w[0]); ix = (int32_t)(uint32_t)w[1]; }
+    }
+    wave_argbest(k, ix, src);
+    o->key = k;
+    o->idx = ix;
+    for (int r = 0; r < 3; ++r) o->a[r] = rl64((int64_t)w[2 + r], src);
+    o->labels = (uint64_t)rl64((int64_t)w[5], src);
+    o->price = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w[6], src));
+    return true;
+}
+
 }  // namespace
 
 // One batch's ordered commit by the whole workgroup (kSpcThreads).  COH: the lists arrive from other
@@ -639,6 +699,25 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                     }
                 }
                 kf = __builtin_amdgcn_readfirstlane(kf);
+                bool rescued = false;
+                RescueOut ro{};
+                if constexpr (COH) {
+                    // the persistent commit (one rank) rescues an exhausted list instead of truncating the batch
+                    if (kf == 3 && A.rescue &&
+                        commit_rescue(A, f, rl64(rc, f), rl64(rm, f), rl64(rp, f), (uint64_t)rl64((int64_t)sel, f),
+                                      m.ti, nT, &ro)) {
+                        if (lane == 0) ++L->stats[4];
+                        const bool ht = wi != kNoIdx;
+                        if (ro.idx != kNoIdx && !(ht && better(wk, wi, ro.key, ro.idx))) {
+                            kf = 1;  // a first touch of a node no candidate list held
+                            rescued = true;
+                            wk = ro.key;
+                            wi = ro.idx;
+                        } else {
+                            kf = ht ? 2 : 0;
+                        }
+                    }
+                }
                 if (kf == 3) {
                     done = f;  // overflow: the batch stops before pod f
                 } else {
@@ -652,7 +731,10 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                         int64_t b0, b1, b2;
                         uint64_t lab;
                         float pr;
-                        if (kf == 1) {  // first touch of list entry qf
+                        if (kf == 1 && rescued) {  // first touch of the rescued node
+                            b0 = ro.a[0]; b1 = ro.a[1]; b2 = ro.a[2]; lab = ro.labels; pr = ro.price;
+                            s = nT++;
+                        } else if (kf == 1) {  // first touch of list entry qf
                             int64_t ra[3];
                             load_rec_state<COH>(A.lists + (size_t)f * K + qf, ra, &lab, &pr);
                             b0 = ra[0]; b1 = ra[1]; b2 = ra[2];
@@ -675,7 +757,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                                 x.sb[0] = b0; x.sb[1] = b1; x.sb[2] = b2;
                                 x.labels = lab; x.price = pr; x.pad = 0;
                                 m.ti[s] = wi;
-                                const int pos = m.HP[qf * 64 + f];
+                                const int pos = rescued ? spc_pos_insert(m.hk, wi) : m.HP[qf * 64 + f];
                                 m.tkc[pos >> 5] |= 1u << (pos & 31);
                             }
                             x.mine = 1;
@@ -748,6 +830,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             L->stats[1] += (done < nb) ? 1 : 0;
             L->stats[2] += placed;
             for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
+            st_coh(&A.ctl->stats[4], (uint64_t)L->stats[4]);  // rescues
             persist_plan(A, done < nb, p0 + done);
         } else {
             A.xout->count = base;

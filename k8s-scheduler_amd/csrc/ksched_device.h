@@ -31,6 +31,19 @@ __device__ __forceinline__ void st_coh(void *p, uint64_t v) {
 __device__ __forceinline__ double ld_coh_f64(const void *p) { return __longlong_as_double((long long)ld_coh(p)); }
 __device__ __forceinline__ void st_coh_f64(void *p, double v) { st_coh(p, (uint64_t)__double_as_longlong(v)); }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// 16-byte sc1 accesses (same valid form: write-through stores, L2-served loads) through a buffer resource over
+// `base` (byte offsets < 2^31): one 16-B record per lane in one request, where two 8-B stores to the same
+// 16 B are two partial-line write requests.  gfx950 buffer aux bit 4 = sc1.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t coh_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st_coh16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 16);
+}
+__device__ __forceinline__ u32x4 ld_coh16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+}
 
 constexpr int kPrioResource = 0;
 constexpr int kPrioPrice = 1;
@@ -62,7 +75,8 @@ __device__ __forceinline__ NodeRec load_row(const NodeRecC *p) {
     return r;
 }
 
-// One candidate of a partial top-K list (score kernels -> merge kernels).
+// One candidate of a partial top-K list (score kernels -> merge kernels).  The persistent pipeline carries a
+// list's predicate count in entry 0's pad (one 16-B store per entry, no separate count word).
 struct alignas(16) Cand {
     double key;
     int32_t idx;  // global node index, kNoIdx = empty slot

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -194,6 +195,7 @@ struct ksched_ctx {
     struct {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
         bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
+        bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
     } diag;
 };
@@ -701,14 +703,15 @@ int enqueue_persistent(ksched_ctx *c) {
     if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
     if (lgp && (info.occ < 1 || (int64_t)lgp->R * (1 + G + M) > (int64_t)(c->cus - kXcds) * info.occ))
         return fail(c, KSCHED_E_INVALID, "local rank group: the ranks' grids do not fit the device together");
-    // workspace: part lists [kPipeLag][B][G][KC] + counts [kPipeLag][B][G] (score(b + kPipeLag) reuses
+    // workspace: part lists [kPipeLag][B][G][KC] with the counts in entry 0's pad (score(b + kPipeLag) reuses
     // batch b's), list ring 4 x (B*K Rec + B fc), XBuf ring
     const size_t part_b = align_up((size_t)kPipeLag * B * G * KC * sizeof(Cand), 256);
-    const size_t cnt_b = align_up((size_t)kPipeLag * B * G * sizeof(int64_t), 256);
+    const size_t cnt_b = 0;
     const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
     const size_t xb = align_up(xbuf_bytes(B), 256);
     const size_t prog_b = align_up((size_t)(G + B + 1) * kProgWords * 8, 256);
-    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b;
+    const size_t resc_b = align_up(rescue_bytes(B), 256);
+    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b + resc_b;
     if (c->pws_bytes < need) {
         if (c->d_pws) hipFree(c->d_pws);
         c->d_pws = nullptr;
@@ -722,12 +725,13 @@ int enqueue_persistent(ksched_ctx *c) {
     a.pods = PodArgs{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
     a.ctl = reinterpret_cast<Ctl *>(c->d_cursor);
     a.part = reinterpret_cast<Cand *>(w);
-    a.part_cnt = reinterpret_cast<int64_t *>(w + part_b);
     a.lring = w + part_b + cnt_b;
     a.lists_bytes = (int64_t)lists_b;
     a.xring = a.lring + 4 * lists_b;
     a.xbuf_bytes = (int64_t)xb;
     a.prog = reinterpret_cast<uint64_t *>(a.xring + 5 * xb);
+    // the rescue of exhausted lists needs the whole node set on this device: one rank only (R > 1 truncates)
+    a.rescue = c->xchg_run ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     c->d_prog = a.prog;
     c->prog_G = G;
     c->prog_rows = R;
@@ -763,6 +767,10 @@ int enqueue_persistent(ksched_ctx *c) {
         a.mdbg = c->d_mdbg;
     }
     hipStream_t sS = c->stream;
+    if (c->diag.poison) {  // read-before-write hunting: stale workspace and LDS become 0xff everywhere
+        HIPCHK(c, hipMemsetAsync(c->d_pws, 0xff, need, sS));
+        a.poison_lds = (int32_t)info.lds;
+    }
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
     HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + 1) * kProgWords * 8, sS));
@@ -908,6 +916,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.merge_stamps = env_int("KSCHED_MERGE_STAMPS", 0) != 0;
     c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
+    c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane
@@ -1047,7 +1056,9 @@ int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) 
     if (!c->d_rx) {
         // uncached: a peer's xGMI stores and this GPU's polls meet in memory, never in a stale L2 line
         HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
-        HIPCHK(c, hipMemset(c->d_rx, 0, bytes));  // tag 0 is never a live tag (epochs start at 1)
+        // tag 0 is never a live tag (epochs start at 1); zeroed in the stream order of this context's kernels
+        HIPCHK(c, hipMemsetAsync(c->d_rx, 0, bytes, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
         c->rx_bytes = bytes;
     }
     if (!c->d_xmin) HIPCHK(c, hipMalloc((void **)&c->d_xmin, sizeof(int32_t)));
@@ -1109,12 +1120,23 @@ int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) {
     const size_t bytes = xchg_ring_bytes(n, c0->B, c0->K);
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
-        if (!c->d_rx) {  // the same ring as xchg_export's (uncached), never IPC-exported
-            HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
-            HIPCHK(c, hipMemset(c->d_rx, 0, bytes));
+        if (c->d_rx && c->rx_bytes < bytes) { hipFree(c->d_rx); c->d_rx = nullptr; }
+        if (!c->d_rx) {
+            // one device, one kernel: the granules are sc1 traffic inside one device's memory (like the score
+            // -> merge lists), so plain device memory serves; xchg_export's rings are uncached because a peer
+            // GPU's xGMI stores and this GPU's polls must meet in memory
+            HIPCHK(c, hipMalloc(&c->d_rx, bytes));
             c->rx_bytes = bytes;
         }
+        // zeroed in the context's stream order (its kernels run on non-blocking streams, which a legacy-stream
+        // hipMemset does not order), and finished before anyone launches
+        HIPCHK(c, hipMemsetAsync(c->d_rx, 0, c->rx_bytes, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
     }
+    // granule tags of this group start at a base no earlier group of this process used: a ring allocated where
+    // an earlier group's ring was can never hold a granule whose tag this group waits for
+    static std::atomic<uint32_t> epoch_bases{0};
+    const uint32_t epoch0 = (epoch_bases.fetch_add(1) + 1u) << 20;
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
         for (int q = 0; q < kMaxXchgRanks; ++q) {
@@ -1123,7 +1145,7 @@ int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) {
         }
         c->lg = g;
         c->xchg_ready = true;
-        c->xchg_epoch = 1;
+        c->xchg_epoch = epoch0;
     }
     return KSCHED_OK;
 }
@@ -1581,8 +1603,17 @@ static int sync_impl(ksched_ctx *c) {
         c->st.batches = h->stats[0];
         c->st.truncations = h->stats[1];
         c->st.placed = h->stats[2];
+        c->st.rescues = h->stats[4];
         c->st.pair_evals = (h->stats[0] + h->stats[3]) * c->persist_B * c->n_local;
         c->persist_stats = false;
+        if (c->d_prog) {  // the score workgroups' exact / scanned row counts (progress words 4, 5)
+            std::vector<uint64_t> w((size_t)kProgWords * c->prog_G);
+            HIPCHK(c, hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost));
+            for (int g = 0; g < c->prog_G; ++g) {
+                c->st.exact_rows += (int64_t)w[(size_t)kProgWords * g + 4];
+                c->st.scan_rows += (int64_t)w[(size_t)kProgWords * g + 5];
+            }
+        }
     }
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));

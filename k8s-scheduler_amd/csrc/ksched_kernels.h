@@ -116,7 +116,24 @@ struct alignas(128) Ctl {
     CtlLine arrive[4];             // score workgroups done with active batch a: G per use of the slot
     CtlLine merged[4];             // merger workgroups done with active batch a: B per use of the slot
     CtlLine committed_x[kCtlReplicas];  // Ctl::committed, one replica per XCD: workgroup w polls w % 8
+    // the rescue of an exhausted candidate list (persistent pipeline, one rank): the commit publishes request
+    // number q in rescue_req, each of the B merger slots scans its share of the nodes and counts its result in
+    // rescue_done (B per request)
+    CtlLine rescue_req;
+    CtlLine rescue_done;
 };
+// The rescue request the commit writes (PersistArgs::rescue; sc1 stores, then Ctl::rescue_req) and the merger
+// slots' results after it: {rc, rm, rp, sel, nT} and the touched set's node indices, then Rec res[B].
+constexpr int kRescueMaxT = 256;  // >= the persistent commit's touched slots (spc_slots<true>() + 1)
+struct alignas(16) RescueReq {
+    int64_t rc, rm, rp;
+    uint64_t sel;
+    int64_t nT;
+    int64_t pad;
+    int64_t ti[kRescueMaxT];
+};
+constexpr size_t kRescueResOff = (sizeof(RescueReq) + 127) / 128 * 128;
+constexpr size_t rescue_bytes(int B) { return kRescueResOff + (size_t)B * sizeof(Rec); }
 
 struct PodArgs {
     const int64_t *rc, *rm, *rp;
@@ -195,9 +212,10 @@ constexpr int msg_words(int K) { return K * kRecWords + 2; }
 struct PersistLocal {
     int64_t plan[kPlanRing];
     int64_t cursor;
-    int64_t stats[5];
+    int64_t stats[5];  // as Ctl::stats; [4] = rescues
     int32_t xcount;   // entries of the previous batch's export
     int32_t xcount2;  // entries of the export of the batch before it (both are inherited: lag kPipeLag)
+    int64_t rseq;     // rescue requests issued this call
 };
 
 struct CommitArgs {
@@ -218,6 +236,10 @@ struct CommitArgs {
     int64_t *cursor_at;     // persistent pipeline: &Ctl::cursor_at[batch % kPlanRing] (else null)
     PersistLocal *loc;      // persistent pipeline (COH): the commit workgroup's LDS control state
     int32_t release;        // COH: also write back the XCD's L2 (agent release) before Ctl::committed
+    char *rescue;           // persistent pipeline, one rank: the rescue request / results (else null: truncate)
+    int32_t rescue_n;       // merger slots serving a rescue (= B)
+    int64_t timeout_ticks;  // bound of the rescue wait
+    int32_t *err;           // device error word (12 = the rescue wait timed out)
 };
 
 // Commit(b) -> score(b + lag) hand-off on the device (lag 2 on the stream pipeline, kPipeLag in k_pipe): the
@@ -353,8 +375,7 @@ struct PersistArgs {
     Ctl *ctl;
     int32_t B, G, rows_per_wg;
     int32_t M;              // merger workgroups (after the G score workgroups): kPipeMergeSlots pod slots each
-    Cand *part;             // [2][B][G][KC]
-    int64_t *part_cnt;      // [2][B][G]
+    Cand *part;             // [kPipeLag][B][G][KC], entry 0's pad = the list's predicate count
     char *lring;            // 4 x {Rec [B][K]; int64 fc[B]}
     int64_t lists_bytes;
     char *xring;            // 4 XBufs + the permanently empty one (slot 4)
@@ -383,11 +404,14 @@ struct PersistArgs {
     // << 32 | low word of the last value a wait saw, busy-time sums}; read by the host when a wait timed out
     // (and by the phase trace)
     uint64_t *prog;
+    char *rescue;           // RescueReq + Rec res[B] (one rank; null: exhausted lists truncate their batch)
+    int32_t poison_lds;     // diagnostics (KSCHED_POISON): bytes of dynamic LDS every workgroup fills with 0xff first
 };
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
-constexpr int kProgWords = 4;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy
+constexpr int kProgWords = 6;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4 rows scored exactly, 5 rows scanned
 enum : int { kProgWaitCommit = 1, kProgScan = 2, kProgArrived = 3, kProgWaitArrive = 4, kProgMerged = 5,
-             kProgWaitMerged = 6, kProgCommitted = 7, kProgIdle = 8, kProgTimedOut = 0x80 };
+             kProgWaitMerged = 6, kProgCommitted = 7, kProgIdle = 8, kProgRescue = 9, kProgWaitRescue = 10,
+             kProgTimedOut = 0x80 };
 __device__ __forceinline__ uint32_t hw_where() {
     uint32_t xcc, hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));

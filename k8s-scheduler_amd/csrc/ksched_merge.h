@@ -300,29 +300,28 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     if (dbg) ts[0] = __builtin_amdgcn_s_memtime();
     const int64_t p0 = A.p0_known ? A.p0v : load_i64<COH>(A.cursor);
     if (p0 < 0 || p0 >= A.P || b >= A.B || p0 + b >= A.P) return;  // uniform over the merging threads
+    static_assert(COH, "merge_pod_fast reads the persistent pipeline's 16-B list records");
     const bool has = tid < A.C_in;
     uint64_t code[KC];
     int32_t idx[KC];
     int n = 0;
     int64_t cnt = 0;
     {
-        const Cand *src = static_cast<const Cand *>(A.in) + ((size_t)b * A.C_in + (has ? tid : 0)) * KC;
+        // one 16-B sc1 load per entry {key, idx, pad}; entry 0's pad is the list's predicate count
+        const __amdgpu_buffer_rsrc_t rs = coh_rsrc(A.in);
+        const uint32_t off = (uint32_t)(((size_t)b * A.C_in + (has ? tid : 0)) * KC * sizeof(Cand));
+        u32x4 w[KC];
+#pragma unroll
+        for (int q = 0; q < KC; ++q) w[q] = ld_coh16(rs, off + (uint32_t)(q * sizeof(Cand)));
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
-            int32_t x;
-            double kq;
-            if (COH) {
-                x = has ? (int32_t)(uint32_t)ld_coh(&src[q].idx) : kNoIdx;
-                kq = has ? ld_coh_f64(&src[q].key) : 0.0;
-            } else {
-                x = has ? src[q].idx : kNoIdx;
-                kq = has ? src[q].key : 0.0;
-            }
+            const int32_t x = has ? (int32_t)w[q].z : kNoIdx;
+            const double kq = __longlong_as_double((long long)(((uint64_t)w[q].y << 32) | w[q].x));
             idx[q] = x;
             code[q] = x == kNoIdx ? 0ull : key_code(kq);
             n += x != kNoIdx;
         }
-        if (has) cnt = load_i64<COH>(A.in_cnt + (size_t)b * A.C_in + tid);
+        cnt = has ? (int64_t)(int32_t)w[0].w : 0;
     }
 #pragma unroll
     for (int q = 0; q < KC; ++q) { sm.code[tid][q] = code[q]; sm.idx[tid][q] = idx[q]; }

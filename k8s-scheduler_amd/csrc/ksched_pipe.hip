@@ -256,6 +256,8 @@ struct alignas(16) MergeCtl {
     unsigned mbar;
     int32_t m_stop;
     int64_t m_p0, m_done;
+    int32_t m_w, pad;             // mwait's outcome (0 held, 1 rescue pending, 2 timed out)
+    unsigned long long m_q;       // the pending rescue request
 };
 template <int KC, int K>
 struct MergeLayout {
@@ -313,6 +315,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     constexpr bool kScreen = PRIO == kPrioResource && F53;
     constexpr int kScreenOffBatches = 16;
     int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
+    int64_t ex_rows = 0, scan_rows = 0;  // tid 0: rows scored exactly / rows scanned (progress words 4, 5)
+    const int64_t Rvalid = (n - g + G - 1) / G;  // rows of this workgroup that hold a node
     int64_t nact = 0;
     int idle = 0;
     unsigned long long early_c = 0;  // wave 0 lane 0: Ctl::committed as read before the last fold
@@ -720,21 +724,19 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
         Cand *part = P.part + (size_t)(b % kPipeLag) * part_elems * KC;  // merge(b) is done before score(b + kPipeLag)
-        int64_t *part_cnt = P.part_cnt + (size_t)(b % kPipeLag) * part_elems;
-        if (folds && pl < P.B && p0 + pl < NP) {  // every lane of the group holds the pod's list: lane src stores entry src
-            Cand *dst = part + ((size_t)pl * G + g) * KC;
-            if (src < KC) {
-                double kk = key[0];
-                int32_t ii = idx[0];
+        if (folds && pl < P.B && p0 + pl < NP && src < KC) {
+            // every lane of the group holds the pod's list: lane src stores entry src as one 16-B record
+            // {key, idx, pad}, entry 0's pad carrying the workgroup's predicate count for the pod
+            double kk = key[0];
+            int32_t ii = idx[0];
 #pragma unroll
-                for (int q = 1; q < KC; ++q) {
-                    kk = src == q ? key[q] : kk;
-                    ii = src == q ? idx[q] : ii;
-                }
-                st_coh(&dst[src].key, (uint64_t)__double_as_longlong(kk));
-                st_coh(&dst[src].idx, (uint64_t)(uint32_t)ii);  // idx + pad (0)
+            for (int q = 1; q < KC; ++q) {
+                kk = src == q ? key[q] : kk;
+                ii = src == q ? idx[q] : ii;
             }
-            if (src == 7) st_coh(part_cnt + (size_t)pl * G + g, (uint64_t)(int64_t)s_cnt[pl]);
+            const uint64_t kb = (uint64_t)__double_as_longlong(kk);
+            const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, src == 0 ? (uint32_t)s_cnt[pl] : 0u};
+            st_coh16(coh_rsrc(part), (uint32_t)((((size_t)pl * G + g) * KC + src) * sizeof(Cand)), v);
         }
         drain_stores();
         sync();  // every wave's stores are drained
@@ -742,6 +744,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
             if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
             if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap) P.trace[b * kTraceCols + 13] = (uint64_t)pc->s_ex;
+            if (lane == 0) { ex_rows += scr ? pc->s_ex : Rvalid; scan_rows += Rvalid; }
             // ---- arrive (the merge waves of workgroups 1 .. B wait for all G) ----
             const int slot = (int)((nact - 1) % 4);
             if (lane == 0) {
@@ -756,6 +759,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         }
         // the next batch's first barrier orders s_cnt / fold reuse after wave 0's reads
     }
+    if (tid == 0 && P.prog) { P.prog[kProgWords * g + 4] = (uint64_t)ex_rows; P.prog[kProgWords * g + 5] = (uint64_t)scan_rows; }
     // every pod is resolved: this workgroup's rows go back to HBM whole (allocatable, cached doubles,
     // reciprocals) for the next call and for ksched_read_nodes
     for (int e = tid; e < R * 6; e += kST) {
@@ -766,12 +770,129 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
 }
 
 // ------------------------------------------------------------------------------------------------
+// The rescue of an exhausted candidate list, merger side (commit side: commit_rescue, ksched_commit.h)
+// ------------------------------------------------------------------------------------------------
+// mtid 0 of a merger slot: wait for *p >= v like poll_ge, serving rescues meanwhile.  0: it holds; 1: a
+// rescue request newer than `served` is pending (*q); 2: timed out (*seen = the last value read).
+__device__ __forceinline__ int poll_ge_or_rescue(const PersistArgs &P, int slot, const unsigned long long *p,
+                                                 unsigned long long v, unsigned long long served,
+                                                 unsigned long long *q, unsigned long long *seen) {
+    const unsigned long long *rq = &P.ctl->rescue_req.v;
+    const bool resc = P.rescue != nullptr;
+    unsigned long long x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (x >= v) { *seen = x; return 0; }
+    const uint64_t t0 = wall_clock64();
+    for (int it = 1;; ++it) {
+        if (resc) {
+            const unsigned long long r = (it & 1023) == 0 ? (unsigned long long)ld_rmw(rq)
+                                                          : __hip_atomic_load(rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (r > served) { *q = r; *seen = x; return 1; }
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if ((it & 1023) == 0) {
+            if (P.prog) __hip_atomic_store(P.prog + kProgWords * slot + 2, (uint64_t)it, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            x = (unsigned long long)ld_rmw(p);
+            if (x >= v) {
+                __hip_atomic_fetch_add(&P.ctl->polls_rmw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                *seen = x;
+                return 0;
+            }
+            if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) { *seen = x; return 2; }
+        } else {
+            x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (x >= v) { *seen = x; return 0; }
+        }
+    }
+}
+
+// One rescue request, by every thread of merger slot `id` (< B): the slot's share of this rank's node rows,
+// [id * chunk, (id + 1) * chunk), at their current state -- the HBM rows, read sc1 (a score workgroup's export
+// apply writes them) -- except the nodes of the request's touched set T, which the commit evaluates itself.
+// Nodes outside T are untouched since the batch's score snapshot (commit(b - 3)); every score workgroup
+// applied that commit's export to HBM before the batch's merges completed, which the commit waited for.  The
+// slot's best eligible (key desc, idx asc) goes to res[id] (sc1, drained) and is counted in Ctl::rescue_done.
+// LDS: the slot's merge scratch, free between merges.  Restated by oracle/cpu_ref.c or_rescue.
+template <int PRIO, int DOM, bool LAB, bool F53, typename Sync>
+__device__ __forceinline__ void serve_rescue(const PersistArgs &P, int id, int mtid, char *scratch, Sync sync) {
+    constexpr int kRH = 1024;  // open-addressed set of T's node indices (|T| <= kRescueMaxT)
+    static_assert(kRH >= 2 * kRescueMaxT, "rescue set");
+    const RescueReq *rq = reinterpret_cast<const RescueReq *>(P.rescue);
+    int32_t *hs = reinterpret_cast<int32_t *>(scratch);
+    double *wk = reinterpret_cast<double *>(scratch + kRH * 4);
+    int32_t *wi = reinterpret_cast<int32_t *>(wk + kMW);
+    const int64_t rc = (int64_t)ld_coh(&rq->rc), rm = (int64_t)ld_coh(&rq->rm), rp = (int64_t)ld_coh(&rq->rp);
+    const uint64_t sel = LAB ? ld_coh(&rq->sel) : 0;
+    const int nT = (int)ld_coh(&rq->nT);
+    auto slot_of = [](int32_t x) { return (int)(((uint32_t)x * 2654435761u) >> 22); };  // log2(kRH) = 10
+    for (int e = mtid; e < kRH; e += kMT) hs[e] = -1;
+    sync();
+    for (int t = mtid; t < nT; t += kMT) {
+        const int32_t x = (int32_t)ld_coh(&rq->ti[t]);
+        for (int h = slot_of(x);; h = (h + 1) & (kRH - 1)) {
+            const int32_t prev = atomicCAS(&hs[h], -1, x);
+            if (prev == -1 || prev == x) break;
+        }
+    }
+    sync();
+    const int64_t n = P.n_local;
+    const int64_t chunk = (n + P.B - 1) / P.B;
+    const int64_t lo = (int64_t)id * chunk, hi = lo + chunk < n ? lo + chunk : n;
+    const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp, y3 = recip(3.0);
+    double bk = -__builtin_inf();
+    int32_t bi = kNoIdx;
+    for (int64_t j = lo + mtid; j < hi; j += kMT) {
+        const int32_t gj = (int32_t)(P.node_offset + j);
+        bool in_t = false;
+        for (int h = slot_of(gj);; h = (h + 1) & (kRH - 1)) {
+            const int32_t x = hs[h];
+            if (x == gj) { in_t = true; break; }
+            if (x == -1) break;
+        }
+        if (in_t) continue;
+        const NodeRec &nd = P.nodes[j];
+        const int64_t a0 = (int64_t)ld_coh(&nd.a[0]), a1 = (int64_t)ld_coh(&nd.a[1]), a2 = (int64_t)ld_coh(&nd.a[2]);
+        const uint64_t lab = LAB ? nd.labels : 0ull;  // labels and prices never change during a call
+        const bool f = fits(rc, rm, rp, sel, a0, a1, a2, lab, LAB);
+        const double f0 = (double)a0, f1 = (double)a1, f2 = (double)a2;
+        double k;
+        if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, a0, a1, a2, f0, f1, f2, recip_or_zero(a0, f0),
+                                          recip_or_zero(a1, f1), recip_or_zero(a2, f2), y3, nd.price, &k) &&
+            better(k, gj, bk, bi)) {
+            bk = k;
+            bi = gj;
+        }
+    }
+    int32_t aux = 0;
+    wave_argbest(bk, bi, aux);
+    if ((mtid & 63) == 0) { wk[mtid >> 6] = bk; wi[mtid >> 6] = bi; }
+    sync();
+    if (mtid == 0) {
+        for (int w = 1; w < kMW; ++w)
+            if (wi[w] != kNoIdx && better(wk[w], wi[w], bk, bi)) { bk = wk[w]; bi = wi[w]; }
+        Rec r{};
+        if (bi != kNoIdx) {
+            const NodeRec &nd = P.nodes[bi - P.node_offset];
+            r.key = bk; r.idx = bi; r.valid = 1;
+            r.a[0] = (int64_t)ld_coh(&nd.a[0]); r.a[1] = (int64_t)ld_coh(&nd.a[1]); r.a[2] = (int64_t)ld_coh(&nd.a[2]);
+            r.labels = nd.labels; r.price = nd.price;
+        } else {
+            r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
+        }
+        store_rec<true>(reinterpret_cast<Rec *>(P.rescue + kRescueResOff) + id, r);
+        drain_stores();
+        __hip_atomic_fetch_add(&P.ctl->rescue_done.v, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // MERGE role (slot id = kMS * merger workgroup + slot, id < B; kMT threads): pods m = id, id + kMS * M, ...
 // of every batch
 // ------------------------------------------------------------------------------------------------
-template <int KC, int K>
+template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>
 __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, const int g) {
     using ML = MergeLayout<KC, K>;
+    static_assert(sizeof(MergeSmem<KC, K, kMT>) >= 1024 * 4 + kMW * 12, "serve_rescue's scratch");
     MergeCtl *pc = reinterpret_cast<MergeCtl *>(sbase);
     MergeSmem<KC, K, kMT> &ms = *reinterpret_cast<MergeSmem<KC, K, kMT> *>(sbase + ML::ctl_bytes);
     uint32_t *s_msg = reinterpret_cast<uint32_t *>(sbase + ML::ctl_bytes + ML::merge_bytes);  // this rank's list
@@ -785,21 +906,39 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
     auto sync = [&]() { role_sync(&pc->mbar, bar, kMW); };
     int64_t nact = 0;
     int idle = 0;
-    for (int64_t b = 0;; ++b) {
-        if (mtid == 0) {
-            int stop = 0;
-            unsigned long long seen = 0;
-            prog_at(P, slot_prog, b, kProgWaitCommit, 0);
-            if (b >= kPipeLag && !spin_ge(P, slot_prog, &ctl->committed_x[g % kCtlReplicas].v,
-                                          (unsigned long long)(b - kPipeLag + 1), &seen)) {
-                set_err(P.err, 6);
-                prog_at(P, slot_prog, b, kProgWaitCommit | kProgTimedOut, seen);
-                stop = 2;
+    unsigned long long served = 0;  // rescue requests this slot has served
+    // a wait of the slot (mtid 0 polls) that serves the commit's rescue requests while it waits; false: timed
+    // out (error errc).  Every path from the read of pc->m_w to its next write passes a role_sync.
+    auto mwait = [&](int64_t b, const unsigned long long *p, unsigned long long v, int errc, int phase) -> bool {
+        for (;;) {
+            if (mtid == 0) {
+                unsigned long long seen = 0, q = 0;
+                prog_at(P, slot_prog, b, phase, 0);
+                const int w = poll_ge_or_rescue(P, slot_prog, p, v, served, &q, &seen);
+                if (w == 2) {
+                    set_err(P.err, errc);
+                    prog_at(P, slot_prog, b, phase | kProgTimedOut, seen);
+                }
+                pc->m_w = w;
+                pc->m_q = q;
             }
+            sync();
+            const int w = pc->m_w;
+            if (w == 0) return true;
+            if (w == 2) return false;
+            if (mtid == 0) prog_at(P, slot_prog, b, kProgRescue, pc->m_q);
+            served = pc->m_q;
+            serve_rescue<PRIO, DOM, LAB, F53>(P, g, mtid, reinterpret_cast<char *>(&ms), sync);
+        }
+    };
+    for (int64_t b = 0;; ++b) {
+        if (b >= kPipeLag && !mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - kPipeLag + 1), 6,
+                                    kProgWaitCommit))
+            return;
+        if (mtid == 0) {
             pc->m_p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
             pc->m_done = b >= kPipeLag ? (int64_t)ld_coh(&ctl->cursor_at[(b - kPipeLag) % kPlanRing]) : 0;
-            if (__hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) stop = 3;
-            pc->m_stop = stop;
+            pc->m_stop = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ? 3 : 0;
         }
         sync();
         if (pc->m_stop) return;
@@ -818,23 +957,13 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         ++nact;
         const int slot = (int)((nact - 1) % 4);
         const unsigned long long use = (unsigned long long)((nact - 1) / 4);
-        if (mtid == 0) {
-            unsigned long long seen = 0;
-            prog_at(P, slot_prog, b, kProgWaitArrive, 0);
-            pc->m_stop = spin_ge(P, slot_prog, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, &seen) ? 0 : 1;
-            if (pc->m_stop) {
-                set_err(P.err, 7);
-                prog_at(P, slot_prog, b, kProgWaitArrive | kProgTimedOut, seen);
-            }
-            if (g == 0) trace_at(P, b, 7);
-        }
-        sync();
-        if (pc->m_stop) return;
+        if (!mwait(b, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, 7, kProgWaitArrive)) return;
+        if (mtid == 0 && g == 0) trace_at(P, b, 7);
         const size_t part_elems = (size_t)P.B * G;
         char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
         MergeArgs ma{};
         ma.in = P.part + (size_t)(b % kPipeLag) * part_elems * KC;
-        ma.in_cnt = P.part_cnt + (size_t)(b % kPipeLag) * part_elems;
+        ma.in_cnt = nullptr;  // the counts travel in entry 0's pad
         ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
         ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
         ma.p0_known = 1; ma.p0v = p0;
@@ -907,6 +1036,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_rmw(&ctl->stats[i]);
         loc.xcount = 0;
         loc.xcount2 = 0;
+        loc.rseq = 0;
     }
     __syncthreads();
     const int cslot = P.G + P.B;  // progress slot
@@ -976,6 +1106,10 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
         ca.dbg = P.cdbg;
         ca.loc = &loc;
+        ca.rescue = P.rescue;  // null for R > 1: an exhausted list truncates its batch there
+        ca.rescue_n = P.B;
+        ca.timeout_ticks = P.timeout_ticks;
+        ca.err = P.err;
         if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged)) {
             if (threadIdx.x == 0) atomicCAS(P.err, 0, 5);
             if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
@@ -1005,6 +1139,10 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
     for (int i = 1; i < kMaxLocalRanks; ++i) r += (i < L.R && (int)blockIdx.x >= L.base[i]) ? 1 : 0;
     const PersistArgs &P = L.P[r];
     const int blk = (int)blockIdx.x - L.base[r];
+    if (P.poison_lds) {  // diagnostics: any LDS read before its write then sees 0xff bytes, not a predecessor's data
+        for (int i = (int)threadIdx.x; i < P.poison_lds / 4; i += kPipeThreads) reinterpret_cast<uint32_t *>(smem)[i] = ~0u;
+        __syncthreads();
+    }
     if (blk == 0) {
 #ifndef KSCHED_PROBE_NO_COMMIT
         commit_role<K, PRIO, DOM, LAB, F53>(P, smem);
@@ -1027,7 +1165,7 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
     if (threadIdx.x % kMT == 0) reinterpret_cast<MergeCtl *>(sbase)->mbar = 0;
     __syncthreads();  // the only workgroup-wide barrier: before the slots part
 #ifndef KSCHED_PROBE_NO_MERGE
-    if (id < P.B) merge_role<KC, K>(P, sbase, id);
+    if (id < P.B) merge_role<KC, K, PRIO, DOM, LAB, F53>(P, sbase, id);
 #endif
 }
 

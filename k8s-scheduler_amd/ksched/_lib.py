@@ -53,7 +53,7 @@ class Stats(C.Structure):
     _fields_ = [("pods", C.c_int64), ("placed", C.c_int64), ("batches", C.c_int64), ("truncations", C.c_int64),
                 ("pair_evals", C.c_int64), ("device_ms", C.c_double), ("kernel_ms", C.c_double * 4),
                 ("kernel_launches", C.c_int64 * 4), ("kernel_pairs", C.c_int64 * 4),
-                ("pipeline", C.c_int64)]
+                ("pipeline", C.c_int64), ("rescues", C.c_int64), ("exact_rows", C.c_int64), ("scan_rows", C.c_int64)]
 
 
 class KschedError(RuntimeError):

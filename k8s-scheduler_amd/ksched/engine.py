@@ -217,7 +217,8 @@ class Engine:
         return dict(pods=s.pods, placed=s.placed, batches=s.batches, truncations=s.truncations,
                     pair_evals=s.pair_evals, device_ms=s.device_ms, kernel_ms=list(s.kernel_ms),
                     kernel_launches=list(s.kernel_launches), kernel_pairs=list(s.kernel_pairs),
-                    pipeline=PIPELINES.get(int(s.pipeline), str(int(s.pipeline))))
+                    pipeline=PIPELINES.get(int(s.pipeline), str(int(s.pipeline))), rescues=s.rescues,
+                    exact_rows=s.exact_rows, scan_rows=s.scan_rows)
 
     def set_timing(self, on: bool, every: int = 0):
         """Sampled per-kernel HIP-event timing for the following calls (every: one batch in N)."""

@@ -556,6 +556,23 @@ typedef struct or_touched {
     int32_t pad2;
 } or_touched;
 
+/* The rescue of an exhausted list (the device's commit asks its merger workgroups for it, ksched_pipe.hip):
+ * the node rows as the batch's score saw them -- the current state of every node the batch's touched set does
+ * not hold -- so the best untouched node can be found by a full scan instead of truncating the batch. */
+typedef struct or_rescue {
+    int64_t n;
+    const int64_t *ac, *am, *ap;
+    const uint64_t *labels;
+    const float *price;
+    int64_t count;  /* rescues performed */
+} or_rescue;
+
+static int64_t commit_batch_impl(const or_opts *o, int32_t K, int64_t nb,
+                                 const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
+                                 const or_rec *lists, const int64_t *fc0,
+                                 or_touched *touched, int32_t *ntouched, int32_t max_touched,
+                                 int32_t *out_idx, double *out_score, int32_t *out_feas, or_rescue *rs);
+
 /* Ordered commit of a batch against merged lists.  Returns the number of pods resolved before the
  * first overflow (>= 1 when nb >= 1).  touched/ntouched carry the nodes committed in this batch.
  * The caller applies touched[].cur to its node state (owners only, when sharded). */
@@ -565,6 +582,16 @@ int64_t or_commit_batch(const or_opts *o, int32_t K, int64_t nb,
                         or_touched *touched, int32_t *ntouched, int32_t max_touched,
                         int32_t *out_idx, double *out_score, int32_t *out_feas)
 {
+    return commit_batch_impl(o, K, nb, rc, rm, rp, sel, lists, fc0, touched, ntouched, max_touched, out_idx,
+                             out_score, out_feas, NULL);
+}
+
+static int64_t commit_batch_impl(const or_opts *o, int32_t K, int64_t nb,
+                                 const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
+                                 const or_rec *lists, const int64_t *fc0,
+                                 or_touched *touched, int32_t *ntouched, int32_t max_touched,
+                                 int32_t *out_idx, double *out_score, int32_t *out_feas, or_rescue *rs)
+{
     int64_t i;
     int use_labels = o->use_labels && sel;
     for (i = 0; i < nb; i++) {
@@ -573,7 +600,7 @@ int64_t or_commit_batch(const or_opts *o, int32_t K, int64_t nb,
         int64_t fc = fc0[i];
         int32_t t, q, cnt = 0, tb = -1, first_untouched = -1;
         double tkey = 0.0;
-        int64_t w = -1;
+        int64_t w = -1, rj = -1;  /* rj: the rescued node (not in the list), when the rescue wins */
         double wkey = 0.0;
         for (t = 0; t < *ntouched; t++) {
             const or_touched *T = &touched[t];
@@ -604,13 +631,43 @@ int64_t or_commit_batch(const or_opts *o, int32_t K, int64_t nb,
             if (tb >= 0) { w = touched[tb].idx; wkey = tkey; }
         } else {
             if (tb >= 0 && cand_better(tkey, touched[tb].idx, L[K - 1].key, L[K - 1].idx)) { w = touched[tb].idx; wkey = tkey; }
-            else return i; /* overflow: the best untouched node may lie beyond the list */
+            else if (!rs) return i; /* overflow: the best untouched node may lie beyond the list */
+            else {
+                /* rescue: the best node outside the touched set over every node, at its current state */
+                int64_t j, bj = -1;
+                double bk = 0.0;
+                int ul = o->use_labels && rs->labels && sel;
+                for (j = 0; j < rs->n; j++) {
+                    double k;
+                    int ft, is_t = 0;
+                    for (t = 0; t < *ntouched; t++) if (touched[t].idx == j) { is_t = 1; break; }
+                    if (is_t) continue;
+                    ft = fits(rc[i], rm[i], rp[i], s, rs->ac[j], rs->am[j], rs->ap[j], ul ? rs->labels[j] : 0, ul);
+                    if (!pair_key(o, ft, rc[i], rm[i], rp[i], rs->ac[j], rs->am[j], rs->ap[j],
+                                  rs->price ? rs->price[j] : 0.f, &k))
+                        continue;
+                    if (bj < 0 || cand_better(k, j, bk, bj)) { bk = k; bj = j; }
+                }
+                rs->count++;
+                if (tb >= 0 && (bj < 0 || cand_better(tkey, touched[tb].idx, bk, bj))) { w = touched[tb].idx; wkey = tkey; }
+                else if (bj >= 0) { w = bj; wkey = bk; rj = bj; }
+            }
         }
         if (w < 0) { out_idx[i] = OR_NO_POSITIVE_SCORE; out_score[i] = 0.0; continue; }
         /* commit */
         {
             int32_t slot = -1;
             for (t = 0; t < *ntouched; t++) if (touched[t].idx == w) { slot = t; break; }
+            if (slot < 0 && rj >= 0) { /* the rescued node: its state from the rows */
+                if (*ntouched >= max_touched) return i;
+                slot = (*ntouched)++;
+                touched[slot].idx = (int32_t)rj;
+                touched[slot].s0[0] = touched[slot].cur[0] = rs->ac[rj];
+                touched[slot].s0[1] = touched[slot].cur[1] = rs->am[rj];
+                touched[slot].s0[2] = touched[slot].cur[2] = rs->ap[rj];
+                touched[slot].labels = rs->labels ? rs->labels[rj] : 0;
+                touched[slot].price = rs->price ? rs->price[rj] : 0.f;
+            }
             if (slot < 0) {
                 const or_rec *u = NULL;
                 for (q = 0; q < cnt; q++) if (L[q].idx == w) { u = &L[q]; break; }
@@ -684,7 +741,7 @@ typedef struct or_xrec { int32_t idx; int64_t sb[3], cur[3]; uint64_t labels; fl
 static int64_t commit_inherit(const or_opts *o, int32_t K, int64_t nb, const int64_t *rc, const int64_t *rm,
                               const int64_t *rp, const uint64_t *sel, const or_rec *lists, const int64_t *fc0,
                               const or_xrec *xin, int32_t nin, or_xrec *xout, int32_t *nout,
-                              int32_t *out_idx, double *out_score, int32_t *out_feas)
+                              int32_t *out_idx, double *out_score, int32_t *out_feas, or_rescue *rs)
 {
     /* touched table: inherited entries first (s0 = state at this batch's snapshot, cur = current) */
     or_touched *T = (or_touched *)malloc(sizeof(or_touched) * (size_t)(nin + nb + 1));
@@ -702,8 +759,8 @@ static int64_t commit_inherit(const or_opts *o, int32_t K, int64_t nb, const int
     {
         /* reuse or_commit_batch's decision rule, but with a pre-filled touched table */
         int32_t before = nt;
-        done = or_commit_batch(o, K, nb, rc, rm, rp, sel, lists, fc0, T, &nt, nin + (int32_t)nb + 1,
-                               out_idx, out_score, out_feas);
+        done = commit_batch_impl(o, K, nb, rc, rm, rp, sel, lists, fc0, T, &nt, nin + (int32_t)nb + 1,
+                                 out_idx, out_score, out_feas, rs);
         /* entries opened by this batch: state at batch start = snapshot state */
         for (t = before; t < nt; t++) memcpy(sb[t], T[t].s0, sizeof(sb[t]));
     }
@@ -767,7 +824,7 @@ int or_schedule_pipelined(const or_opts *o, int32_t K, int32_t B, int64_t n,
         if (s != cursor) { if (stats) stats[2]++; continue; } /* invalidated speculation */
         done = commit_inherit(o, K, nb, rc + s, rm + s, rp + s, sel ? sel + s : NULL, recs, fc,
                               X[(b + 2) % 3], b >= 1 ? nx[(b + 2) % 3] : 0, X[cb], &nx[cb],
-                              out_idx + s, out_score + s, out_feas + s);
+                              out_idx + s, out_score + s, out_feas + s, NULL);
         cursor = s + done;
         if (done < nb) resync = 1;
         if (stats) { stats[0]++; stats[1] += done < nb; }
@@ -793,12 +850,31 @@ int or_schedule_pipelined(const or_opts *o, int32_t K, int32_t B, int64_t n,
  * that committed it) and its current state (after the newest); plan(b) for b < L is b * B, commit(b)
  * plans batch b + L (its cursor after a truncation, else plan(b + L - 1) + B), and a batch whose plan is
  * not the cursor is skipped.  Test infrastructure: tests/test_oracle.py checks it against or_schedule. */
+int or_schedule_lagged_rescue(const or_opts *o, int32_t K, int32_t B, int32_t L, int32_t rescue, int64_t n,
+                              int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
+                              int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp,
+                              const uint64_t *sel, int32_t *out_idx, double *out_score, int32_t *out_feas,
+                              int64_t *stats);
+
 int or_schedule_lagged(const or_opts *o, int32_t K, int32_t B, int32_t L, int64_t n,
                        int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
                        int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
                        int32_t *out_idx, double *out_score, int32_t *out_feas, int64_t *stats)
 {
+    return or_schedule_lagged_rescue(o, K, B, L, 0, n, ac, am, ap, labels, price, p, rc, rm, rp, sel, out_idx,
+                                     out_score, out_feas, stats);
+}
+
+/* rescue = 1: an exhausted list is rescued by a full scan of the untouched nodes (or_rescue) instead of
+ * truncating the batch -- the device's persistent commit since round 4; stats[3] = rescues. */
+int or_schedule_lagged_rescue(const or_opts *o, int32_t K, int32_t B, int32_t L, int32_t rescue, int64_t n,
+                              int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
+                              int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp,
+                              const uint64_t *sel, int32_t *out_idx, double *out_score, int32_t *out_feas,
+                              int64_t *stats)
+{
     enum { RING = 8 };
+    or_rescue rs = {n, ac, am, ap, labels, price, 0};
     or_xrec *X[RING], *inh;
     int32_t nx[RING];
     int64_t plan[RING];
@@ -846,7 +922,7 @@ int or_schedule_lagged(const or_opts *o, int32_t K, int32_t B, int32_t L, int64_
             }
         }
         done = commit_inherit(o, K, nb, rc + s, rm + s, rp + s, sel ? sel + s : NULL, recs, fc, inh, nin,
-                              X[cb], &nx[cb], out_idx + s, out_score + s, out_feas + s);
+                              X[cb], &nx[cb], out_idx + s, out_score + s, out_feas + s, rescue ? &rs : NULL);
         cursor = s + done;
         nxt = plan[(b + L - 1) % RING];
         nxt = done < nb ? cursor : (nxt < 0 ? -1 : nxt + B);
@@ -863,6 +939,7 @@ int or_schedule_lagged(const or_opts *o, int32_t K, int32_t B, int32_t L, int64_
             ac[j] = X[ab][i].cur[0]; am[j] = X[ab][i].cur[1]; ap[j] = X[ab][i].cur[2];
         }
     }
+    if (stats) stats[3] = rs.count;
     for (k = 0; k < RING; k++) free(X[k]);
     free(inh); free(recs); free(fc);
     return OR_OK;

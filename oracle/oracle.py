@@ -169,8 +169,10 @@ def schedule_pipelined(cl, K: int, B: int, n_pods=None):
     return oi, os_, of, (ac, am, ap), dict(batches=int(st[0]), truncations=int(st[1]), skipped=int(st[2]))
 
 
-def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None):
-    """CPU model of the persistent pipeline at lag `lag` (the device runs 3): cpu_ref.c or_schedule_lagged."""
+def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None, rescue: bool = False):
+    """CPU model of the persistent pipeline at lag `lag` (the device runs 3): cpu_ref.c or_schedule_lagged_rescue;
+    rescue=True resolves an exhausted candidate list by a full scan of the untouched nodes (the device's commit)
+    instead of truncating the batch."""
     ac, am, ap = (np.ascontiguousarray(x, dtype=np.int64).copy() for x in (cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))
     p = cl.n_pods if n_pods is None else int(n_pods)
     rc, rm, rp = (np.ascontiguousarray(x[:p], dtype=np.int64) for x in (cl.req_cpu, cl.req_mem, cl.req_pods))
@@ -178,16 +180,18 @@ def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None):
     sel = None if cl.selector is None else np.ascontiguousarray(cl.selector[:p], dtype=np.uint64)
     pr = None if cl.price is None else np.ascontiguousarray(cl.price, dtype=np.float32)
     oi = np.empty(p, np.int32); os_ = np.empty(p, np.float64); of = np.empty(p, np.int32)
-    st = np.zeros(3, np.int64)
+    st = np.zeros(4, np.int64)
     o = _opts(cl.priority, cl.domain, cl.use_labels)
-    r = lib().or_schedule_lagged(C.byref(o), C.c_int32(K), C.c_int32(B), C.c_int32(lag), C.c_int64(ac.shape[0]),
+    r = lib().or_schedule_lagged_rescue(C.byref(o), C.c_int32(K), C.c_int32(B), C.c_int32(lag), C.c_int32(int(rescue)),
+                                        C.c_int64(ac.shape[0]),
                                  _p(ac, C.c_int64), _p(am, C.c_int64), _p(ap, C.c_int64),
                                  _p(lab, C.c_uint64), _p(pr, C.c_float), C.c_int64(p),
                                  _p(rc, C.c_int64), _p(rm, C.c_int64), _p(rp, C.c_int64), _p(sel, C.c_uint64),
                                  _p(oi, C.c_int32), _p(os_, C.c_double), _p(of, C.c_int32), _p(st, C.c_int64))
     if r != 0:
         raise RuntimeError(f"or_schedule_lagged failed: {r}")
-    return oi, os_, of, (ac, am, ap), dict(batches=int(st[0]), truncations=int(st[1]), skipped=int(st[2]))
+    return oi, os_, of, (ac, am, ap), dict(batches=int(st[0]), truncations=int(st[1]), skipped=int(st[2]),
+                                           rescues=int(st[3]))
 
 
 def local_topk(opts, K, offset, ac, am, ap, labels, price, rc, rm, rp, sel):

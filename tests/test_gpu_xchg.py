@@ -19,8 +19,11 @@ pytestmark = pytest.mark.gpu
 def run_local(cl, world, calls=2):
     from ksched.dist import make_local_xchg_group
     ranks = make_local_xchg_group(cl, world, device=0, topk=16, batch=64)
-    for e, _ in ranks:
+    for e, (lo, hi) in ranks:
         assert e.xchg_ready, "exchange join failed"
+        st0 = e.read_nodes()
+        assert all(np.array_equal(st0[k], a[lo:hi]) for k, a in enumerate((cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))), \
+            f"rank node state after load differs from the input (shard {lo}:{hi})"
         e.save_state()
     out = [None] * world
     errs = []
@@ -33,7 +36,8 @@ def run_local(cl, world, calls=2):
                 e.restore_state()
                 oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
                 st = e.stats()
-                res.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"]))
+                res.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"],
+                            st["exact_rows"]))
             out[r] = (res, e.read_nodes())
         except Exception as ex:  # surfaced below
             errs.append((r, repr(ex)))
@@ -58,9 +62,18 @@ def test_xchg_ranks_match_oracle(gpu_available, oracle_mod, cfg, nn, pp, world):
     want = oracle_mod.schedule(cl, nthreads=8)
     out = run_local(cl, world)
     for r in range(world):
-        for oi, osb, of, pipe, nb, ntr in out[r][0]:
+        for c, (oi, osb, of, pipe, nb, ntr, exr) in enumerate(out[r][0]):
             assert pipe == "persistent", f"rank {r} ran the {pipe} pipeline"
-            assert np.array_equal(oi, want[0]), f"rank {r}: assignments differ at {np.nonzero(oi != want[0])[0][:5]}"
+            if not np.array_equal(oi, want[0]):
+                w1 = oracle_mod.schedule(cl, nthreads=1)[0]
+                agree = [all(np.array_equal(out[0][0][k][0], out[q][0][k][0]) for q in range(world))
+                         for k in range(len(out[0][0]))]
+                bad = np.nonzero(oi != want[0])[0][:5]
+                raise AssertionError(
+                    f"rank {r} call {c} ({nb} batches, {ntr} truncated, {exr} exact rows): assignments differ at {bad} "
+                    f"(got {oi[bad]}, oracle {want[0][bad]}; 1-thread oracle equal to the 8-thread one: "
+                    f"{np.array_equal(w1, want[0])}; ranks agree per call: {agree}; "
+                    f"other calls: {[(x[4], x[5], x[6], int((x[0] != want[0]).sum())) for x in out[r][0]]})")
             assert np.array_equal(osb, want[1].view(np.int64)), f"rank {r}: score bits differ"
             assert np.array_equal(of, want[2]), f"rank {r}: feasible counts differ"
     got = [np.concatenate([out[r][1][k] for r in range(world)]) for k in range(3)]

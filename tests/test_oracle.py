@@ -201,3 +201,34 @@ def test_lagged_restatement_skip_accounting(oracle_mod, lag):
     assert st["truncations"] > 10
     assert st["skipped"] <= (lag - 1) * st["truncations"]
     assert st["skipped"] >= 0.9 * (lag - 1) * st["truncations"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_lagged_rescue_equals_sequential(oracle_mod, seed):
+    """The device's rescue of an exhausted candidate list (a full scan of the nodes outside the batch's touched
+    set, at their current state) restated at lag 3: the same sequential result with no truncation at all, on
+    the high-conflict clusters where the truncating pipeline truncates most."""
+    from ksched import cluster
+    combos = [(0, 0, False), (0, 1, False), (1, 1, False), (0, 1, True), (1, 1, True), (0, 0, True)]
+    pr, dm, lb = combos[seed]
+    cl = cluster.random_small(91 + seed, n_nodes=96, n_pods=500, priority=pr, domain=dm, use_labels=lb)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    for K, B in ((4, 16), (8, 64), (16, 64)):
+        plain = oracle_mod.schedule_lagged(cl, K, B, 3)[4]
+        bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, K, B, 3, rescue=True)
+        assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+        assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+        for a, b in zip(st, bst):
+            assert np.array_equal(a, b)
+        assert stats["truncations"] == 0 and stats["skipped"] == 0
+        assert stats["rescues"] >= plain["truncations"]  # every truncation became a rescue (or more: later batches differ)
+
+
+def test_lagged_rescue_c4_like(oracle_mod):
+    """A c4-shaped cluster (the bench's distribution, fewer nodes): rescue on, still the sequential result."""
+    from ksched import cluster
+    cl = cluster.make_cluster("c4", n_nodes=2000, n_pods=3000)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, 16, 64, 3, rescue=True)
+    assert np.array_equal(oi, bi) and np.array_equal(of, bf) and np.array_equal(os_.view(np.int64), bs.view(np.int64))
+    assert stats["truncations"] == 0
