@@ -258,10 +258,15 @@ def main():
         # VALU figures are the SQ passes' counts per launch over the launch's pairs (a wave64 instruction
         # covers 64 pairs: lane = pod); the call is bound by the lagged dependency chain
         # score -> merge -> commit -> score of a later batch.
+        # the screened scan scores only its survivors in f64: the algorithmic figure counts every
+        # pair of the sequential semantics; exact_rows_frac says how many of them the kernel evaluated in f64
+        exact_frac = (st.get("exact_rows", 0) / st["scan_rows"]) if st.get("scan_rows") else None
         lim = {
             "what": "lagged dependency chain (score -> merge -> commit -> later score); VALU issue latency",
             "fp64_tflops_algorithmic": value / max(world, 1) * FLOPS_PER_PAIR / 1e12,
             "fp64_peak_tflops": FP64_VALU_PEAK_TFLOPS,
+            "exact_rows_frac": exact_frac,
+            "fp64_tflops_executed": (value / max(world, 1) * FLOPS_PER_PAIR / 1e12 * exact_frac) if exact_frac else None,
         }
         if pmc and score_pairs_per_launch > 0:
             for f, name in (("_SQ_INSTS_VALU", "valu"), ("_F64", "fp64_valu"), ("_SQ_INSTS_SALU", "salu"),
@@ -296,6 +301,7 @@ def main():
         "placed_pods_per_sec": placed * args.steps / elapsed,
         "batches_per_step": int(st["batches"]),
         "truncated_batches_per_step": int(st["truncations"]),
+        "rescued_lists_per_step": int(st.get("rescues", 0)),
         "kernel_avg_ms": fam_share,
         "roofline": roof,
     }

@@ -453,6 +453,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     double my_score = 0.0;
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
     int nT = nin, done = nb, W = 64;
+    int nresc = 0;  // wave 0: rescues of this batch
     int64_t placed = 0, nrounds = 0, nfail = 0, niters = 0;
     if (wave == 0) {
         fcc = pj ? (int32_t)(fc0v + m.dfacc[lane]) : 0;
@@ -703,9 +704,10 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                 RescueOut ro{};
                 if constexpr (COH) {
                     // the persistent commit (one rank) rescues an exhausted list instead of truncating the batch
-                    if (kf == 3 && A.rescue &&
+                    if (kf == 3 && A.rescue && nresc < A.rescue_max &&
                         commit_rescue(A, f, rl64(rc, f), rl64(rm, f), rl64(rp, f), (uint64_t)rl64((int64_t)sel, f),
                                       m.ti, nT, &ro)) {
+                        ++nresc;
                         if (lane == 0) ++L->stats[4];
                         const bool ht = wi != kNoIdx;
                         if (ro.idx != kNoIdx && !(ht && better(wk, wi, ro.key, ro.idx))) {

@@ -196,6 +196,8 @@ struct ksched_ctx {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
         bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
+        int rescue_max = 2;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
+                                 // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
     } diag;
 };
@@ -731,7 +733,8 @@ int enqueue_persistent(ksched_ctx *c) {
     a.xbuf_bytes = (int64_t)xb;
     a.prog = reinterpret_cast<uint64_t *>(a.xring + 5 * xb);
     // the rescue of exhausted lists needs the whole node set on this device: one rank only (R > 1 truncates)
-    a.rescue = c->xchg_run ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
+    a.rescue = c->xchg_run || c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
+    a.rescue_max = c->diag.rescue_max;
     c->d_prog = a.prog;
     c->prog_G = G;
     c->prog_rows = R;
@@ -917,6 +920,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
     c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
+    c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 2);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane

@@ -238,6 +238,7 @@ struct CommitArgs {
     int32_t release;        // COH: also write back the XCD's L2 (agent release) before Ctl::committed
     char *rescue;           // persistent pipeline, one rank: the rescue request / results (else null: truncate)
     int32_t rescue_n;       // merger slots serving a rescue (= B)
+    int32_t rescue_max;     // rescues per batch; the next exhausted list truncates the batch
     int64_t timeout_ticks;  // bound of the rescue wait
     int32_t *err;           // device error word (12 = the rescue wait timed out)
 };
@@ -406,6 +407,7 @@ struct PersistArgs {
     uint64_t *prog;
     char *rescue;           // RescueReq + Rec res[B] (one rank; null: exhausted lists truncate their batch)
     int32_t poison_lds;     // diagnostics (KSCHED_POISON): bytes of dynamic LDS every workgroup fills with 0xff first
+    int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
 };
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
 constexpr int kProgWords = 6;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4 rows scored exactly, 5 rows scanned

@@ -1108,6 +1108,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         ca.loc = &loc;
         ca.rescue = P.rescue;  // null for R > 1: an exhausted list truncates its batch there
         ca.rescue_n = P.B;
+        ca.rescue_max = P.rescue_max;
         ca.timeout_ticks = P.timeout_ticks;
         ca.err = P.err;
         if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged)) {

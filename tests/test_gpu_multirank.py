@@ -73,10 +73,10 @@ def test_rank_group_equals_sequential(gpu_available, oracle_mod, R, case):
     assert len({(o[4]["batches"], o[4]["truncations"], o[4]["placed"]) for o in out}) == 1
 
 
-@pytest.mark.parametrize("R", [2, 8])
+@pytest.mark.parametrize("R", [2, 4, 8])
 def test_rank_group_c4_full_nodes(gpu_available, oracle_mod, R):
-    """c4 node-sharded at the FULL 100k nodes (R = 2: 50k per rank; R = 8: the 8-GPU split, 12.5k per rank),
-    a 5k-pod prefix against the sequential oracle, final state included."""
+    """c4 node-sharded at the FULL 100k nodes (R = 2, 4, 8: BASELINE's 2/4/8-GPU splits, 50k / 25k / 12.5k per
+    rank), a 5k-pod prefix against the sequential oracle, final state included."""
     from ksched import cluster
     cl = cluster.make_cluster("c4", n_pods=5000)
     assert cl.n_nodes == 100_000
@@ -119,3 +119,16 @@ def test_one_rank_at_node_offset(gpu_available, oracle_mod):
             oi, os_, of = e.schedule(shard.req_cpu, shard.req_mem, shard.req_pods)
             st = e.read_nodes()
         assert_same((oi, os_, of, st), (wi, want[1], want[2], want[3]), f"offset {lo} {kw}")
+
+
+def test_rank_group_c5_full_nodes_r8(gpu_available, oracle_mod):
+    """c5 -- BASELINE's 8-GPU config: 200k heterogeneous near-full nodes, label bitsets, feasible-only argmax --
+    at its FULL node count split over R = 8 ranks (25k nodes each), a 5k-pod prefix against the oracle."""
+    from ksched import cluster
+    cl = cluster.make_cluster("c5", n_pods=5000)
+    assert cl.n_nodes == 200_000 and cl.use_labels
+    want = oracle_mod.schedule(cl, nthreads=16)
+    out, final = run_group(cl, 8, topk=16, batch=64)
+    for r in range(8):
+        assert_same(out[r][:3] + ((),), want, f"c5 R=8 rank {r}")
+    assert_same((want[0], want[1], want[2], final), want, "c5 R=8 final state")

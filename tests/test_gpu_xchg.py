@@ -55,7 +55,7 @@ def run_local(cl, world, calls=2):
 
 
 @pytest.mark.parametrize("cfg,nn,pp,world", [("c3", 24000, 3000, 2), ("c5hc", 20000, 3000, 2), ("c4", 30000, 2500, 3),
-                                             ("c4", 100000, 2500, 2), ("c5", 40000, 2000, 4)])
+                                             ("c4", 100000, 2500, 2), ("c5", 40000, 2000, 4), ("c4", 100000, 5000, 4)])
 def test_xchg_ranks_match_oracle(gpu_available, oracle_mod, cfg, nn, pp, world):
     from ksched import cluster
     cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)

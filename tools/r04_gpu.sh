@@ -14,6 +14,13 @@ step() {  # step <name> <seconds> <cmd...>
   tail -3 "gpurun_out/$name.log"
   return $rc
 }
+soft() {  # soft <name> <seconds> <cmd...>: a step whose failure (rc 1: a failed test) does not end the call;
+          # a crash, abort or time limit (rc >= 124) does
+  step "$@"
+  local rc=$?
+  if [ $rc -ge 124 ]; then exit $rc; fi
+  return 0
+}
 trace() {  # trace <name> [bench args]: the c4 phase trace with the raw per-batch stamps dumped
   local name=$1; shift
   KSCHED_PERSIST_TRACE=1 KSCHED_COMMIT_STAMPS=1 KSCHED_MERGE_STAMPS=1 KSCHED_TRACE_DUMP=gpurun_out/$name.bin \
@@ -36,6 +43,15 @@ case "$1" in
       step exit_$v 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_exit_$v -o run \
         -- python3 tools/exit_probe.py $v || exit 1
     done
+    ;;
+  s2)
+    KSCHED_POISON=1 soft xchg_poison 200 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+      tests/test_gpu_xchg.py -k c4-100000 &&
+    soft xchg_all 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_xchg.py &&
+    trace trace_c4 &&
+    KSCHED_RESCUE_MAX=0 soft bench_c4_norescue 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+    soft bench_c4 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
+    KSCHED_RESCUE_MAX=2 soft bench_c4_resc2 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
     ;;
   trace) shift; trace "$@" ;;
   *) "$@" ;;
