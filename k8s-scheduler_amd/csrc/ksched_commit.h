@@ -51,7 +51,6 @@ static_assert(sizeof(SpcSlot) == 72, "SpcSlot");
 
 struct SpcSmem {
     int32_t *hk;      // open-addressed table: node index per position (-1 = empty)
-    int32_t *ps;      // prologue only (aliases S): slot of each inherited node's table position
     int64_t *s0;      // prologue only (aliases D): [inherited slot][3] state at this batch's score snapshot
     double *iy;       // prologue only (aliases GS): [inherited slot][6] current state as doubles, reciprocals
     int32_t *HP;      // [K][64] table position of list entry (q, pod); kSpcInvalid for no entry
@@ -74,6 +73,8 @@ struct SpcSmem {
                       // step 1 only (aliases pbk/pbx, which steps 2-3 use)
     uint64_t *GS;     // [64 pods][kGS] each pod's guessed entry: state a[3], labels, price, and the state after
                       // the pod's commit n[3] with its (double) and refined reciprocals (computed once, lane = pod)
+    // persistent commit: the slots of the older export (batch b - 2) are keyed by the merger workgroups
+    int16_t *x2s;     // [64] slot of that export's entry e (-1: the node is also in export(b - 1): no slot)
 };
 
 __device__ __forceinline__ uint32_t spc_hash(int32_t idx) {
@@ -175,8 +176,10 @@ __device__ __forceinline__ bool commit_rescue(const CommitArgs &A, int f, int64_
         A.loc->rseq = (int64_t)q;
         __hip_atomic_store(&A.ctl->rescue_req.v, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned long long seen = 0;
+        const uint64_t t0 = A.trace_row ? wall_clock64() : 0;
         ok = poll_ge(&A.ctl->rescue_done.v, q * (unsigned long long)A.rescue_n, A.timeout_ticks, &A.ctl->polls_rmw,
                      &seen) ? 1 : 0;
+        if (A.trace_row) A.trace_row[17] += wall_clock64() - t0;  // time the rescues kept the commit waiting
         if (!ok) atomicCAS(A.err, 0, 12);
     }
     ok = __builtin_amdgcn_readfirstlane(ok);
@@ -290,8 +293,8 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
         m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
+        m.x2s = reinterpret_cast<int16_t *>(p); p += 64 * sizeof(int16_t);
         m.D = reinterpret_cast<int8_t *>(p);
-        m.ps = reinterpret_cast<int32_t *>(m.S);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
         m.s0 = reinterpret_cast<int64_t *>(m.D);
         m.iy = reinterpret_cast<double *>(m.GS);
@@ -335,8 +338,8 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     const int n1 = COH ? L->xcount : A.xin->count;  // <= 64 each
     const int n2 = LAG3 ? L->xcount2 : 0;
     XRec xi{};
-    if (wave == 0 && lane < n1) xi = load_xrec<COH>(&A.xin->e[lane]);
-    if (LAG3 && wave == 1 && lane < n2) xi = load_xrec<COH>(&A.xin2->e[lane]);
+    if (wave == 0 && lane < n1) xi = load_xrec<COH>(A.xin->e, lane);
+    if (LAG3 && wave == 1 && lane < n2) xi = load_xrec<COH>(A.xin2->e, lane);
     for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
     if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
     __syncthreads();
@@ -350,13 +353,15 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.ti[lane] = xi.idx;
         stage_state(m.iy + lane * 6, xi.cur);
         const int h = spc_pos_insert(m.hk, xi.idx);
-        if (LAG3) m.ps[h] = lane;
         atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
     }
     int nin = n1;
     if constexpr (LAG3) {
-        // slots [n1, nin): nodes only the batch before the previous one committed; a node both committed
-        // keeps the previous batch's slot with the older start state as its snapshot state
+        // slots [n1, nin): nodes only the batch before the previous one committed (a node both committed keeps
+        // the previous batch's slot).  Their keys and predicate deltas come from the merger workgroups, which
+        // computed them for every entry of that export while this batch merged (inherit_x2_keys,
+        // ksched_pipe.hip): the predicate deltas of the two exports add up (an entry's start state in the newer
+        // export is its state after the older one), so the older export's duplicates need no correction here.
         __syncthreads();
         if (wave == 1) {
             bool fresh = false;
@@ -367,18 +372,15 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                 fresh = !existed;
             }
             const uint64_t fm = __ballot(fresh);
-            if (lane < n2) {
-                const int e = fresh ? n1 + __popcll(fm & ((1ull << lane) - 1ull)) : m.ps[h];
-                for (int r = 0; r < 3; ++r) m.s0[e * 3 + r] = xi.sb[r];
-                if (fresh) {
-                    SpcSlot &x = m.T[e];
-                    x.idx = xi.idx; x.mine = 0;
-                    for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
-                    x.labels = xi.labels; x.price = xi.price; x.pad = 0;
-                    m.ti[e] = xi.idx;
-                    stage_state(m.iy + e * 6, xi.cur);
-                    atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
-                }
+            const int e = n1 + __popcll(fm & ((1ull << lane) - 1ull));
+            m.x2s[lane] = (lane < n2 && fresh) ? (int16_t)e : (int16_t)-1;
+            if (lane < n2 && fresh) {
+                SpcSlot &x = m.T[e];
+                x.idx = xi.idx; x.mine = 0;
+                for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+                x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+                m.ti[e] = xi.idx;
+                atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
             }
             if (lane == 0) m.ctl[3] = n1 + __popcll(fm);
         }
@@ -387,6 +389,8 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     } else {
         __syncthreads();
     }
+    // the slots whose keys this workgroup computes: all inherited slots at lag 2, the newer export's at lag 3
+    const int nkey = LAG3 ? n1 : nin;
 
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
@@ -397,7 +401,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         int dfl = 0;
         double pk = -__builtin_inf();
         int32_t pi = kNoIdx, ps = -1;
-        for (int t = wave; t < nin; t += kSpcWaves) {
+        for (int t = wave; t < nkey; t += kSpcWaves) {
             const SpcSlot &x = m.T[t];
             const int64_t *x0 = m.s0 + t * 3;
             const bool f0 = fits(rc, rm, rp, sel, x0[0], x0[1], x0[2], x.labels, LAB);
@@ -429,6 +433,21 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         t_start = t;
     }
     if constexpr (COH) load_lists();
+    // the merger's key columns of the older export's slots (LAG3, batch >= 2): element (pod j, entry e) of
+    // inh keys[batch % 4] into S[j][slot of e], loaded while the list entries are in flight
+    constexpr int kX2Per = 64 * 64 / kSpcThreads + (64 * 64 % kSpcThreads != 0);
+    double x2v[LAG3 ? kX2Per : 1];
+    const bool x2on = LAG3 && A.batch >= 2 && n2 > 0;
+    const double *x2col = LAG3 ? reinterpret_cast<const double *>(A.inh + (size_t)4 * A.B * 32) +
+                                     (size_t)(A.batch % 4) * A.B * 64
+                               : nullptr;
+    if constexpr (LAG3) {
+#pragma unroll
+        for (int u = 0; u < kX2Per; ++u) {
+            const int i = tid + u * kSpcThreads;
+            x2v[u] = (x2on && i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) ? ld_coh_f64(x2col + i) : 0.0;
+        }
+    }
 #pragma unroll
     for (int u = 0; u < kHeadPer; ++u) {
         const int e = tid + u * kSpcThreads;
@@ -440,6 +459,16 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             m.LK[q * 64 + j] = key;
             m.LI[q * 64 + j] = idx;
             m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
+        }
+    }
+    if constexpr (LAG3) {
+#pragma unroll
+        for (int u = 0; u < kX2Per; ++u) {
+            const int i = tid + u * kSpcThreads;
+            if (x2on && i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) {
+                const int sl = m.x2s[i & 63];
+                if (sl >= 0) m.S[(size_t)(i >> 6) * kSpcRow + sl] = x2v[u];
+            }
         }
     }
     __syncthreads();
@@ -454,9 +483,20 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
     int nT = nin, done = nb, W = 64;
     int nresc = 0;  // wave 0: rescues of this batch
-    int64_t placed = 0, nrounds = 0, nfail = 0, niters = 0;
+    int64_t placed = 0, nrounds = 0, nfail = 0, niters = 0, nseq = 0;
     if (wave == 0) {
-        fcc = pj ? (int32_t)(fc0v + m.dfacc[lane]) : 0;
+        int64_t ds2 = 0;
+        double xk = -__builtin_inf();
+        int32_t xix = kNoIdx, xe = -1;
+        if (LAG3 && A.batch >= 2 && n2 > 0 && pj) {  // the merger's summary: {sum of deltas, best key, idx | entry}
+            const uint64_t *sm = reinterpret_cast<const uint64_t *>(A.inh + ((size_t)(A.batch % 4) * A.B + lane) * 32);
+            ds2 = (int64_t)ld_coh(sm);
+            const uint64_t w2 = ld_coh(sm + 2);
+            xk = __longlong_as_double((long long)ld_coh(sm + 1));
+            xix = (int32_t)(uint32_t)w2;
+            xe = (int32_t)(w2 >> 32);
+        }
+        fcc = pj ? (int32_t)(fc0v + m.dfacc[lane] + ds2) : 0;
         cut = cut0;
 #pragma unroll
         for (int q = 0; q < K; ++q) cv += m.LI[q * 64 + lane] != kNoIdx;  // valid entries form a prefix
@@ -465,6 +505,20 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             const int64_t x = m.pbx[w * 64 + lane];
             const int32_t xi = (int32_t)(uint32_t)x;
             if (k != -__builtin_inf() && better(k, xi, rbk, rbi)) { rbk = k; rbi = xi; rbs = (int32_t)(x >> 32); }
+        }
+        if (LAG3 && xix != kNoIdx) {
+            if (m.x2s[xe] >= 0) {  // the best entry has a slot of its own
+                if (better(xk, xix, rbk, rbi)) { rbk = xk; rbi = xix; rbs = m.x2s[xe]; }
+            } else {
+                // (rare) its node is also in the newer export, whose current state supersedes this key: the best
+                // of the entries that do have a slot, from the merger's key column
+                for (int e = 0; e < n2; ++e) {
+                    if (m.x2s[e] < 0) continue;
+                    const double k = Srow[m.x2s[e]];
+                    const int32_t xi = m.ti[m.x2s[e]];
+                    if (k != -__builtin_inf() && better(k, xi, rbk, rbi)) { rbk = k; rbi = xi; rbs = m.x2s[e]; }
+                }
+            }
         }
         if (lane == 0) { m.ctl[0] = 0; m.ctl[2] = 0; }
     }
@@ -638,7 +692,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             const bool valid = (kind == 0 && !guessed_commit) || (kind == 1);
             const bool inw = lane >= c && lane < cend;
             const uint64_t bad = __ballot(inw && !valid);
-            const int f = bad ? (int)__builtin_ctzll(bad) : cend;
+            int f = bad ? (int)__builtin_ctzll(bad) : cend;
             // confirm [c, f)
             const bool conf = lane >= c && lane < f;
             if (conf) {
@@ -666,10 +720,17 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                 ++nfail;
                 // resolve pod f exactly (its inputs are exact: every pod before it is confirmed)
                 int kf = __builtin_amdgcn_readlane(kind, f);
-                const int32_t fcf = __builtin_amdgcn_readlane(fcj, f);
+                int32_t fcf = __builtin_amdgcn_readlane(fcj, f);
                 double wk = readlane_f64(tk, f);
                 int32_t wi = __builtin_amdgcn_readlane(ti, f);
                 int s = __builtin_amdgcn_readlane(ts, f);
+                const int fr = f;  // the round's first failure
+                // A pod whose answer is a node the batch already touched (kind 2) made the guesses after it
+                // void; where that happens pods tend to follow the same node, so the pods after it are resolved
+                // one by one here (the same exact step, the probe of kind 4) for as long as their answers keep
+                // being touched nodes, instead of a guess round (all waves, ~15 us) per pod.  A first touch or
+                // an overflow hands back to the guess rounds.
+                for (;;) {
                 int qf = -1;
                 if (kf == 4) {
                     // first list entry of pod f not in T (guesses before f are confirmed, later ones void)
@@ -782,7 +843,17 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
                         }
                     }
                 }
-                W = 2 * (f - c + 1);
+                if (kf != 2 || f + 1 >= nb) break;
+                // the next pod, exactly: every pod before it is resolved, rbk/fcc are current
+                ++f;
+                ++nseq;
+                fcf = __builtin_amdgcn_readlane(fcc, f);
+                kf = fcf == 0 ? 0 : 4;
+                wk = readlane_f64(rbk, f);
+                wi = __builtin_amdgcn_readlane(rbi, f);
+                s = __builtin_amdgcn_readlane(rbs, f);
+                }
+                W = 2 * (fr - c + 1);
                 W = W < 4 ? 4 : (W > 64 ? 64 : W);
                 c = f + 1;
             } else {
@@ -798,11 +869,14 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     }
     if (wave != 0) return true;
 
-    if (lane < done) {
-        A.out.idx[p0 + lane] = my_idx;
-        A.out.score[p0 + lane] = my_score;
-        A.out.feas[p0 + lane] = my_feas;
-    }
+    auto store_out = [&]() {
+        if (lane < done) {
+            A.out.idx[p0 + lane] = my_idx;
+            A.out.score[p0 + lane] = my_score;
+            A.out.feas[p0 + lane] = my_feas;
+        }
+    };
+    if (!COH) store_out();
     // export this batch's commits (wave-ordered compaction)
     int base = 0;
     for (int t0 = 0; t0 < nT; t0 += 64) {
@@ -817,7 +891,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
             o.labels = x.labels; o.price = x.price; o.pad2 = 0;
             const int slot = base + __popcll(mask & ((1ull << lane) - 1));
-            store_xrec<COH>(&A.xout->e[slot], o);
+            store_xrec<COH>(A.xout->e, slot, o);
         }
         base += __popcll(mask);
     }
@@ -827,12 +901,9 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             L->xcount2 = L->xcount;
             L->xcount = base;
             L->cursor = p0 + done;
-            st_coh(&A.ctl->cursor, (uint64_t)(p0 + done));
             L->stats[0] += 1;
             L->stats[1] += (done < nb) ? 1 : 0;
             L->stats[2] += placed;
-            for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
-            st_coh(&A.ctl->stats[4], (uint64_t)L->stats[4]);  // rescues
             persist_plan(A, done < nb, p0 + done);
         } else {
             A.xout->count = base;
@@ -842,14 +913,28 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             add_i64<COH>(&A.ctl->stats[2], placed);
             plan_after_commit<COH>(A, done < nb, p0 + done);
         }
+        if (A.trace_row)  // rounds | rescues << 16 | resolved pods << 24 | failed guesses << 32 | pods resolved one by one << 48
+            A.trace_row[16] = (uint64_t)nrounds | (uint64_t)nresc << 16 | (uint64_t)done << 24 | (uint64_t)nfail << 32 |
+                              (uint64_t)nseq << 48;
         if (A.dbg) {
             A.dbg[12] += nrounds; A.dbg[13] += nfail; A.dbg[14] += 1; A.dbg[5] += niters;
             A.dbg[0] += t_pro; A.dbg[1] += t_s1; A.dbg[2] += t_s2; A.dbg[3] += t_s3;
+            if (A.trace_row) { A.trace_row[18] = t_pro; A.trace_row[19] = t_s1; A.trace_row[20] = t_s2; A.trace_row[21] = t_s3; }
             A.dbg[4] += __builtin_amdgcn_s_memtime() - t_start;
             A.dbg[6] += t_pre;
         }
     }
     publish_committed<COH>(A);  // wave 0 made every global store of this batch
+    if (COH) {
+        // persistent pipeline: the outputs, the cursor and the counters are read by the host after the kernel
+        // (and by the next call's commit), by no workgroup of this one -- off the hand-off's critical path
+        store_out();
+        if (lane == 0) {
+            st_coh(&A.ctl->cursor, (uint64_t)L->cursor);
+            for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
+            st_coh(&A.ctl->stats[4], (uint64_t)L->stats[4]);  // rescues
+        }
+    }
     return true;
 }
 
@@ -857,12 +942,11 @@ template <int K, int NT = kSpcThreads, bool LAG3 = false>
 constexpr size_t spc_lds_bytes() {
     return (size_t)64 * (spc_slots<LAG3>() + 1) * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 +
            spc_slots<LAG3>() * sizeof(SpcSlot) + (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 +
-           spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 64;
+           spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 2 + 64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
-// the prologue's aliases: the node -> slot map in S, the inherited snapshot states in D
-static_assert((size_t)64 * 129 * 8 >= kSpcHash * 4 && 64 * 64 >= 128 * 3 * 8 && 64 * kGS * 8 >= 128 * 6 * 8,
-              "SpcSmem prologue aliases");
+// the prologue's aliases: the inherited snapshot states in D, their staged doubles in GS
+static_assert(64 * 64 >= 128 * 3 * 8 && 64 * kGS * 8 >= 128 * 6 * 8, "SpcSmem prologue aliases");
 static_assert((size_t)(kSpcThreads / 64) * 64 * 16 >= kSpcHash * 4 && (kPipeThreads / 64) * 64 * 16 >= kSpcHash * 4,
               "SpcSmem::own aliases pbk/pbx");
 

@@ -713,7 +713,8 @@ int enqueue_persistent(ksched_ctx *c) {
     const size_t xb = align_up(xbuf_bytes(B), 256);
     const size_t prog_b = align_up((size_t)(G + B + 1) * kProgWords * 8, 256);
     const size_t resc_b = align_up(rescue_bytes(B), 256);
-    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b + resc_b;
+    const size_t inh_b = align_up(inh_bytes(B), 256);
+    const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b + resc_b + inh_b;
     if (c->pws_bytes < need) {
         if (c->d_pws) hipFree(c->d_pws);
         c->d_pws = nullptr;
@@ -735,6 +736,7 @@ int enqueue_persistent(ksched_ctx *c) {
     // the rescue of exhausted lists needs the whole node set on this device: one rank only (R > 1 truncates)
     a.rescue = c->xchg_run || c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     a.rescue_max = c->diag.rescue_max;
+    a.inh = reinterpret_cast<char *>(a.prog) + prog_b + resc_b;
     c->d_prog = a.prog;
     c->prog_G = G;
     c->prog_rows = R;

@@ -32,31 +32,58 @@ struct alignas(8) Touched {
 static_assert(sizeof(Touched) == 144, "Touched layout");
 
 // Nodes committed by one batch, handed to the next batch's commit (which scored against a snapshot
-// one batch older) and to the apply kernel that writes them into the node rows.
-struct alignas(8) XRec {
+// one batch older) and to the apply kernel that writes them into the node rows.  80 B: five 16-byte chunks
+// {idx, pad, cur0 | cur1, cur2 | sb0, sb1 | sb2, labels | price, pad2, -}, so the persistent pipeline moves a
+// record in 16-byte sc1 accesses, and a score workgroup's export apply (idx + current state) in the first two.
+struct alignas(16) XRec {
     int32_t idx;
     int32_t pad;
-    int64_t sb[3];    // state before the batch (= the next batch's snapshot state)
     int64_t cur[3];   // state after the batch
+    int64_t sb[3];    // state before the batch (= the next batch's snapshot state)
     uint64_t labels;
     float price;
     int32_t pad2;
+    int64_t pad3;
 };
-static_assert(sizeof(XRec) == 72, "XRec layout");
+static_assert(sizeof(XRec) == 80, "XRec layout");
+
+// entry i of the array at (wave-uniform) e: one buffer resource for the wave, the lane's record by offset (a
+// per-lane base would make the resource divergent, which the compiler serialises lane by lane)
+template <bool COH>
+__device__ __forceinline__ XRec load_xrec(const XRec *e, int i) {
+    if constexpr (!COH) {
+        return e[i];
+    } else {
+        const __amdgpu_buffer_rsrc_t r = coh_rsrc(e);
+        const uint32_t off = (uint32_t)i * (uint32_t)sizeof(XRec);
+        u32x4 c[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) c[k] = ld_coh16(r, off + 16u * k);
+        auto w64 = [](uint32_t lo, uint32_t hi) { return (int64_t)(((uint64_t)hi << 32) | lo); };
+        XRec o;
+        o.idx = (int32_t)c[0].x; o.pad = (int32_t)c[0].y;
+        o.cur[0] = w64(c[0].z, c[0].w); o.cur[1] = w64(c[1].x, c[1].y); o.cur[2] = w64(c[1].z, c[1].w);
+        o.sb[0] = w64(c[2].x, c[2].y); o.sb[1] = w64(c[2].z, c[2].w); o.sb[2] = w64(c[3].x, c[3].y);
+        o.labels = (uint64_t)w64(c[3].z, c[3].w);
+        o.price = __uint_as_float(c[4].x); o.pad2 = (int32_t)c[4].y; o.pad3 = 0;
+        return o;
+    }
+}
 
 template <bool COH>
-__device__ __forceinline__ XRec load_xrec(const XRec *p) {
+__device__ __forceinline__ void store_xrec(XRec *e, int i, const XRec &o) {
     if constexpr (!COH) {
-        return *p;
+        e[i] = o;
     } else {
-        const uint64_t *w = reinterpret_cast<const uint64_t *>(p);
-        XRec o;
-        const uint64_t w0 = ld_coh(w), w8 = ld_coh(w + 8);
-        o.idx = (int32_t)(uint32_t)w0; o.pad = (int32_t)(uint32_t)(w0 >> 32);
-        for (int r = 0; r < 3; ++r) { o.sb[r] = (int64_t)ld_coh(w + 1 + r); o.cur[r] = (int64_t)ld_coh(w + 4 + r); }
-        o.labels = ld_coh(w + 7);
-        o.price = __uint_as_float((uint32_t)w8); o.pad2 = (int32_t)(uint32_t)(w8 >> 32);
-        return o;
+        const __amdgpu_buffer_rsrc_t r = coh_rsrc(e);
+        const uint32_t b = (uint32_t)i * (uint32_t)sizeof(XRec);
+        auto lo = [](int64_t v) { return (uint32_t)(uint64_t)v; };
+        auto hi = [](int64_t v) { return (uint32_t)((uint64_t)v >> 32); };
+        st_coh16(r, b, u32x4{(uint32_t)o.idx, (uint32_t)o.pad, lo(o.cur[0]), hi(o.cur[0])});
+        st_coh16(r, b + 16, u32x4{lo(o.cur[1]), hi(o.cur[1]), lo(o.cur[2]), hi(o.cur[2])});
+        st_coh16(r, b + 32, u32x4{lo(o.sb[0]), hi(o.sb[0]), lo(o.sb[1]), hi(o.sb[1])});
+        st_coh16(r, b + 48, u32x4{lo(o.sb[2]), hi(o.sb[2]), lo((int64_t)o.labels), hi((int64_t)o.labels)});
+        st_coh16(r, b + 64, u32x4{__float_as_uint(o.price), (uint32_t)o.pad2, 0u, 0u});
     }
 }
 
@@ -65,22 +92,10 @@ __device__ __forceinline__ void add_i64(int64_t *p, int64_t v) {
     if (COH) st_coh(p, (uint64_t)((int64_t)ld_coh(p) + v)); else *p += v;
 }
 
-template <bool COH>
-__device__ __forceinline__ void store_xrec(XRec *p, const XRec &o) {
-    if constexpr (!COH) {
-        *p = o;
-    } else {
-        uint64_t *w = reinterpret_cast<uint64_t *>(p);
-        st_coh(w, (uint64_t)(uint32_t)o.idx | ((uint64_t)(uint32_t)o.pad << 32));
-        for (int r = 0; r < 3; ++r) { st_coh(w + 1 + r, (uint64_t)o.sb[r]); st_coh(w + 4 + r, (uint64_t)o.cur[r]); }
-        st_coh(w + 7, o.labels);
-        st_coh(w + 8, (uint64_t)__float_as_uint(o.price) | ((uint64_t)(uint32_t)o.pad2 << 32));
-    }
-}
-
-struct alignas(8) XBuf {
+struct alignas(16) XBuf {
     int32_t count;
-    int32_t pad;
+    int32_t pad;      // the persistent pipeline's batch tag
+    int64_t pad2;
     XRec e[1];        // [2 * B] follow
 };
 
@@ -239,8 +254,10 @@ struct CommitArgs {
     char *rescue;           // persistent pipeline, one rank: the rescue request / results (else null: truncate)
     int32_t rescue_n;       // merger slots serving a rescue (= B)
     int32_t rescue_max;     // rescues per batch; the next exhausted list truncates the batch
+    const char *inh;        // persistent commit: the mergers' keys of the older export (inherit_x2_keys), else null
     int64_t timeout_ticks;  // bound of the rescue wait
     int32_t *err;           // device error word (12 = the rescue wait timed out)
+    uint64_t *trace_row;    // KSCHED_PERSIST_TRACE: this batch's trace row (else null)
 };
 
 // Commit(b) -> score(b + lag) hand-off on the device (lag 2 on the stream pipeline, kPipeLag in k_pipe): the
@@ -316,7 +333,7 @@ __device__ __forceinline__ void plan_after_commit(const CommitArgs &A, bool trun
     store_i64<COH>(A.plan2, nx);
 }
 
-constexpr size_t xbuf_bytes(int B) { return 8 + (size_t)2 * B * sizeof(XRec); }
+constexpr size_t xbuf_bytes(int B) { return 16 + (size_t)2 * B * sizeof(XRec); }
 
 // FailedScheduling diagnostics of a whole schedule call (ksched_explain.hip).
 struct ExplainArgs {
@@ -408,7 +425,11 @@ struct PersistArgs {
     char *rescue;           // RescueReq + Rec res[B] (one rank; null: exhausted lists truncate their batch)
     int32_t poison_lds;     // diagnostics (KSCHED_POISON): bytes of dynamic LDS every workgroup fills with 0xff first
     int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
+    // the merger slots' keys of their pod against the entries of export(b - 2), which commit(b) inherits:
+    // [4 batches][B] summaries {sum of predicate deltas, best key, best idx | entry << 32, -} then [4][B][64] keys
+    char *inh;
 };
+constexpr size_t inh_bytes(int B) { return (size_t)4 * B * 32 + (size_t)4 * B * 64 * 8; }
 // progress phases (PersistArgs::prog); kProgWords 8-byte words per workgroup
 constexpr int kProgWords = 6;  // 0 phase, 1 where/seen, 2 heartbeat, 3 busy, 4 rows scored exactly, 5 rows scanned
 enum : int { kProgWaitCommit = 1, kProgScan = 2, kProgArrived = 3, kProgWaitArrive = 4, kProgMerged = 5,
@@ -478,7 +499,8 @@ constexpr size_t xchg_ring_bytes(int R, int B, int K) { return (size_t)4 * R * B
 // all ranks meet on the device and agree on the minimum of a small value (tag: this call's epoch0)
 hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hipStream_t s);
 // trace columns: score start (WG 0 past its wait), last arrival, last merge done, commit start, commit end
-constexpr int kTraceCols = 16;
+constexpr int kTraceCols = 22;  // 0-15 stamps (col 13: exact rows), 16 the commit's counters, 17 its rescue waits,
+                                // 18-21 its prologue / guess / evaluate / check cycles (KSCHED_COMMIT_STAMPS)
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }

@@ -344,7 +344,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             stop = __builtin_amdgcn_readfirstlane(stop);
             int64_t p0v = 0, donev = 0;
             int errv = 0, nxv = 0;
-            uint64_t w0 = 0, w4 = 0, w5 = 0, w6 = 0;
+            u32x4 x0 = {0u, 0u, 0u, 0u}, x1 = {0u, 0u, 0u, 0u};  // entry chunks {idx, pad, cur0} {cur1, cur2}
             const XBuf *xb =
                 reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= kPipeLag ? b - kPipeLag : 0) % 4) * P.xbuf_bytes);
             if (lane == 0) {
@@ -359,25 +359,28 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 const uint64_t hdr = ld_coh(&xb->count);  // one address: one request for the wave
                 nxv = (uint32_t)(hdr >> 32) == (uint32_t)(b - kPipeLag) ? (int)(uint32_t)hdr : 0;
                 if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
-                    const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[lane]);
-                    w0 = ld_coh(w); w4 = ld_coh(w + 4); w5 = ld_coh(w + 5); w6 = ld_coh(w + 6);
+                    const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);  // uniform base, the lane's entry by offset
+                    const uint32_t o = (uint32_t)lane * (uint32_t)sizeof(XRec);
+                    x0 = ld_coh16(rs, o); x1 = ld_coh16(rs, o + 16);
                 }
             }
-            auto apply = [&](uint64_t x0, uint64_t x4, uint64_t x5, uint64_t x6) {
-                const int64_t j = (int64_t)(int32_t)(uint32_t)x0 - P.node_offset;  // local row
+            auto apply = [&](const u32x4 &c0, const u32x4 &c1) {
+                const int64_t j = (int64_t)(int32_t)c0.x - P.node_offset;  // local row
                 if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
-                set_row(rows + j / G, (int64_t)x4, (int64_t)x5, (int64_t)x6);
-                if (P.screen_ok)
-                    ysq[j / G] = make_float4(screen_recip((int64_t)x4), screen_recip((int64_t)x5), screen_recip((int64_t)x6), 0.0f);
+                const int64_t a0 = (int64_t)(((uint64_t)c0.w << 32) | c0.z), a1 = (int64_t)(((uint64_t)c1.y << 32) | c1.x),
+                              a2 = (int64_t)(((uint64_t)c1.w << 32) | c1.z);
+                set_row(rows + j / G, a0, a1, a2);
+                if (P.screen_ok) ysq[j / G] = make_float4(screen_recip(a0), screen_recip(a1), screen_recip(a2), 0.0f);
                 // the mergers read a candidate's state from its HBM row (sc1)
-                st_coh(&P.nodes[j].a[0], x4);
-                st_coh(&P.nodes[j].a[1], x5);
-                st_coh(&P.nodes[j].a[2], x6);
+                st_coh(&P.nodes[j].a[0], (uint64_t)a0);
+                st_coh(&P.nodes[j].a[1], (uint64_t)a1);
+                st_coh(&P.nodes[j].a[2], (uint64_t)a2);
             };
-            if (lane < nxv) apply(w0, w4, w5, w6);
+            if (lane < nxv) apply(x0, x1);
             for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
-                const uint64_t *w = reinterpret_cast<const uint64_t *>(&xb->e[e]);
-                apply(ld_coh(w), ld_coh(w + 4), ld_coh(w + 5), ld_coh(w + 6));
+                const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);
+                const uint32_t o = (uint32_t)e * (uint32_t)sizeof(XRec);
+                apply(ld_coh16(rs, o), ld_coh16(rs, o + 16));
             }
             if (lane == 0) {
                 pc->s_p0 = p0v;
@@ -885,6 +888,51 @@ __device__ __forceinline__ void serve_rescue(const PersistArgs &P, int id, int m
     }
 }
 
+// Pod m of batch b (p0 + m) against the nodes batch b - 2 committed (its export, ring slot (b - 2) % 4): the
+// keys at their current state, the predicate deltas since b's snapshot and the best entry -- what commit(b)
+// would otherwise compute for those inherited slots on its own critical path (commit_spc_batch, LAG3).  Wave 0
+// of the merger slot, lane = export entry; commit(b - 2) is done (the caller waited).  The key column goes to
+// inh keys[b % 4][m][0, n2), the summary to inh summary[b % 4][m]: {sum of deltas, best key, best idx | entry
+// << 32} (entry -1: none eligible).  Restated by oracle/cpu_ref.c commit_inherit (the two exports' deltas add).
+template <int PRIO, int DOM, bool LAB, bool F53>
+__device__ __forceinline__ void inherit_x2_keys(const PersistArgs &P, int64_t b, int m, int64_t pod, int mtid) {
+    if (mtid >= 64) return;
+    const int lane = mtid;
+    const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b - 2) % 4) * P.xbuf_bytes);
+    const uint64_t hdr = ld_coh(&xb->count);
+    const int n2 = (uint32_t)(hdr >> 32) == (uint32_t)(b - 2) ? (int)(uint32_t)hdr : 0;
+    const int64_t rc = P.pods.rc[pod], rm = P.pods.rm[pod], rp = P.pods.rp[pod];
+    const uint64_t sel = LAB ? P.pods.sel[pod] : 0ull;
+    double k = -__builtin_inf();
+    int32_t ix = kNoIdx;
+    int64_t d = 0;
+    double *keys = reinterpret_cast<double *>(P.inh + (size_t)4 * P.B * 32) + ((size_t)(b % 4) * P.B + m) * 64;
+    if (lane < n2) {
+        const XRec x = load_xrec<true>(xb->e, lane);
+        const bool f0 = fits(rc, rm, rp, sel, x.sb[0], x.sb[1], x.sb[2], x.labels, LAB);
+        const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
+        d = (int64_t)f1 - (int64_t)f0;
+        const double c0 = (double)x.cur[0], c1 = (double)x.cur[1], c2 = (double)x.cur[2];
+        double kk;
+        if (pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, (double)rc, (double)rm, (double)rp, x.cur[0], x.cur[1],
+                                          x.cur[2], c0, c1, c2, recip_or_zero(x.cur[0], c0), recip_or_zero(x.cur[1], c1),
+                                          recip_or_zero(x.cur[2], c2), recip(3.0), x.price, &kk)) {
+            k = kk;
+            ix = x.idx;
+        }
+        st_coh_f64(keys + lane, k);
+    }
+    d = wave_sum_i64(d);
+    int32_t src = lane;
+    wave_argbest(k, ix, src);
+    if (lane == 0) {
+        uint64_t *sm = reinterpret_cast<uint64_t *>(P.inh + ((size_t)(b % 4) * P.B + m) * 32);
+        st_coh(sm, (uint64_t)d);
+        st_coh(sm + 1, (uint64_t)__double_as_longlong(k));
+        st_coh(sm + 2, (uint64_t)(uint32_t)ix | (uint64_t)(uint32_t)(ix == kNoIdx ? -1 : src) << 32);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // MERGE role (slot id = kMS * merger workgroup + slot, id < B; kMT threads): pods m = id, id + kMS * M, ...
 // of every batch
@@ -1003,6 +1051,12 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
                 if (pc->m_stop) return;
                 if (mtid < 64) rank_merge_msgs<K>(s_all, RR, ma.out_rec + (size_t)m * K, ma.out_fc + m);
             }
+            // the pod's keys against the older inherited export (commit(b - 2) done: usually long since)
+            if (P.inh && b >= 2 && p0 + m < NP) {
+                if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit))
+                    return;
+                inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid);
+            }
             drain_stores();
             sync();  // every merge wave's stores drained before the count; LDS free for the next pod
             if (mtid == 0) {
@@ -1105,10 +1159,12 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         ca.batch = b;
         ca.cursor_at = &ctl->cursor_at[b % kPlanRing];
         ca.dbg = P.cdbg;
+        ca.trace_row = (P.trace && b < P.trace_cap) ? P.trace + b * kTraceCols : nullptr;
         ca.loc = &loc;
         ca.rescue = P.rescue;  // null for R > 1: an exhausted list truncates its batch there
         ca.rescue_n = P.B;
         ca.rescue_max = P.rescue_max;
+        ca.inh = P.inh;
         ca.timeout_ticks = P.timeout_ticks;
         ca.err = P.err;
         if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged)) {

@@ -9,6 +9,13 @@ variants: torch   torch only (one kernel)
           ksched  + libksched: one small batched schedule, context destroyed explicitly
           leak    + libksched: the same, context left to the interpreter's teardown
           oracle  + the OpenMP oracle (the check leg's checker)
+          load    + libksched: a context created and destroyed, no kernel launched
+          stream  + libksched: the batched schedule on the stream pipeline (plain launches only)
+          exact   + libksched: the exact mode (one cooperative launch of k_exact)
+          notorch libksched's batched schedule (persistent, cooperative) in a process that never imports torch:
+                  libksched then runs on /opt/rocm's HIP runtime instead of the one bundled with torch
+          reset   notorch + hipDeviceReset after the context is destroyed (before any exit handler)
+          treset  ksched (with torch) + hipDeviceReset after the context is destroyed
 """
 import atexit
 import os
@@ -27,14 +34,24 @@ def dump_maps(v):
 def main():
     v = sys.argv[1]
     atexit.register(dump_maps, v)
-    import torch
-    x = torch.ones(1024, device="cuda")
-    print("torch sum", float(x.sum()), flush=True)
+    if v not in ("notorch", "reset"):
+        import torch
+        x = torch.ones(1024, device="cuda")
+        print("torch sum", float(x.sum()), flush=True)
     if v == "torch":
         return
-    from ksched import MODE_BATCHED, Engine, cluster
+    from ksched import MODE_BATCHED, MODE_EXACT, Engine, cluster
     cl = cluster.make_cluster("c3", n_nodes=4000, n_pods=300)
-    e = Engine(mode=MODE_BATCHED, topk=16, batch=64, device=0)
+    if v == "load":
+        Engine(mode=MODE_BATCHED, topk=16, batch=64, device=0).close()
+        print("ksched context created and destroyed", flush=True)
+        return
+    kw = dict(mode=MODE_BATCHED, topk=16, batch=64)
+    if v == "stream":
+        kw["pipeline"] = 1  # KSCHED_PIPELINE_STREAM
+    elif v == "exact":
+        kw = dict(mode=MODE_EXACT)
+    e = Engine(device=0, **kw)
     e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods)
     oi, _, _ = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods)
     print("ksched placed", int((oi >= 0).sum()), e.stats()["pipeline"], flush=True)
@@ -46,6 +63,10 @@ def main():
         e.close()
     else:
         globals()["_leaked"] = e
+    if v in ("reset", "treset"):
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")  # the runtime libksched is bound to (already loaded)
+        print("hipDeviceSynchronize", hip.hipDeviceSynchronize(), "hipDeviceReset", hip.hipDeviceReset(), flush=True)
 
 
 if __name__ == "__main__":

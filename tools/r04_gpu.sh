@@ -39,7 +39,7 @@ case "$1" in
     step pytest_all 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/
     ;;
   exitprobe)  # one variant per step; the first that faults at exit ends the chain (tools/exit_probe.py)
-    for v in torch ksched oracle leak; do
+    for v in ${EXIT_VARIANTS:-torch ksched oracle leak}; do
       step exit_$v 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_exit_$v -o run \
         -- python3 tools/exit_probe.py $v || exit 1
     done
@@ -52,6 +52,14 @@ case "$1" in
     KSCHED_RESCUE_MAX=0 soft bench_c4_norescue 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
     soft bench_c4 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline &&
     KSCHED_RESCUE_MAX=2 soft bench_c4_resc2 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline
+    ;;
+  s3)
+    step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+    step pytest_pipe 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py \
+      -k "persistent or golden or edge or full_size_c3" &&
+    step pytest_xchg 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_xchg.py &&
+    trace trace_c4 &&
+    step bench_c4 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline
     ;;
   trace) shift; trace "$@" ;;
   *) "$@" ;;

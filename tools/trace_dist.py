@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-batch distributions of the persistent pipeline's phase stamps (KSCHED_TRACE_DUMP raw file: [cap][16]
-u64 wall-clock stamps at 100 MHz, the columns of print_persist_trace in ksched_engine.hip).  The stderr summary
+u64: wall-clock stamps at 100 MHz and the commit's counters in column 16, the columns of print_persist_trace in ksched_engine.hip).  The stderr summary
 gives means; a mean can hide a few long stalls, so this prints percentiles and the stalls.
 
   python tools/trace_dist.py gpurun_out/trace_c4.bin [lag=3]
@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-COLS = 16
+COLS = 22
 
 
 def main():
@@ -45,8 +45,32 @@ def main():
     order = np.argsort(-per)[:8]
     for i in order:
         bb = b[i]
+        c = int(t[bb, 16])
         print(f"  batch {bb}: period {per[i]:.1f} us | score {us(t[bb, 1] - t[bb, 0]):.1f} merge {us(t[bb, 2] - t[bb, 1]):.1f}"
-              f" to-commit {us(t[bb, 3] - t[bb, 2]):.1f} commit {us(t[bb, 4] - t[bb, 3]):.1f}")
+              f" to-commit {us(t[bb, 3] - t[bb, 2]):.1f} commit {us(t[bb, 4] - t[bb, 3]):.1f} | rounds {c & 0xffff}"
+              f" rescues {(c >> 16) & 0xff} (waited {us(t[bb, 17]):.1f} us) done {(c >> 24) & 0xff} failed {(c >> 32) & 0xffff}"
+              f" one-by-one {c >> 48} | kcycles pro {t[bb, 18] / 1e3:.1f} guess {t[bb, 19] / 1e3:.1f} eval {t[bb, 20] / 1e3:.1f}"
+              f" check {t[bb, 21] / 1e3:.1f}")
+    cc = t[b, 16]
+    rounds, resc, done = cc & 0xffff, (cc >> 16) & 0xff, (cc >> 24) & 0xff
+    seq = cc >> 48
+    print(f"pods resolved one by one: {seq.sum()} ({seq.sum() / max(len(b), 1):.2f} per batch)")
+    cm = us((t[b, 4] - t[b, 3]).astype(np.float64))
+    rw = us(t[b, 17].astype(np.float64))
+    print(f"rescue waits: {rw.sum() / 1e3:.2f} ms in total, {us(float(t[b, 17].sum())) / max(int(resc.sum()), 1):.1f} us per rescue")
+    print("commit time by rescues in the batch:")
+    for r in range(int(resc.max()) + 1 if len(resc) else 0):
+        s = resc == r
+        if s.any():
+            print(f"  {r} rescues: {s.sum()} batches, commit mean {cm[s].mean():.1f} p50 {np.median(cm[s]):.1f} max {cm[s].max():.1f} us,"
+                  f" rounds mean {rounds[s].mean():.2f}, resolved {done[s].mean():.1f}")
+    print("commit time by rounds (kcycles per batch: prologue / guess / evaluate / check):")
+    for lo, hi in ((0, 1), (1, 2), (2, 3), (3, 5), (5, 10), (10, 1 << 16)):
+        s = (rounds >= lo) & (rounds < hi)
+        if s.any():
+            kc = [t[b[s], c].mean() / 1e3 for c in (18, 19, 20, 21)]
+            print(f"  rounds [{lo},{hi}): {s.sum()} batches, commit mean {cm[s].mean():.1f} max {cm[s].max():.1f} us, total"
+                  f" {cm[s].sum() / 1e3:.2f} ms | {kc[0]:.1f} / {kc[1]:.1f} / {kc[2]:.1f} / {kc[3]:.1f}")
     # which phase of the chain is the long one when the period is long
     chain = us((t[b, 4] - t[b - lag, 4]).astype(np.float64))
     print(f"chain (commit(b-L) end -> commit(b) end): mean {chain.mean():.1f} p50 {np.median(chain):.1f} us = "
