@@ -196,6 +196,8 @@ struct ksched_ctx {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
         bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
+        bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
+                                    // (same residency check; profiled runs: DESIGN.md section 6.1)
         int rescue_max = 2;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
                                  // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
@@ -811,7 +813,8 @@ int enqueue_persistent(ksched_ctx *c) {
                 hipError_t le = hipSuccess;
                 for (int r = 0; r < g->R && le == hipSuccess; ++r)
                     if (r != me) le = hipStreamWaitEvent(sS, g->ready[r], 0);
-                if (le == hipSuccess) le = launch_pipe(g->kc, g->k, g->prio, g->dom, g->lab, g->f53, g->L, 1, nullptr, sS);
+                if (le == hipSuccess) le = launch_pipe(g->kc, g->k, g->prio, g->dom, g->lab, g->f53, g->L, c->diag.plain_launch ? 2 : 1,
+                                                             nullptr, sS);
                 if (le == hipSuccess) le = hipEventRecord(g->done, sS);
                 g->launch_err = le;
             });
@@ -821,7 +824,7 @@ int enqueue_persistent(ksched_ctx *c) {
         HIPCHK(c, hipStreamWaitEvent(sS, g->done, 0));  // (a no-op on the launching rank's own stream)
         e = hipSuccess;
     } else {
-        e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, L, 1, nullptr, sS);
+        e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, L, c->diag.plain_launch ? 2 : 1, nullptr, sS);
     }
     if (e == hipErrorCooperativeLaunchTooLarge && !c->xchg_run) {  // the stream pipeline runs instead
         if (c->diag.debug) fprintf(stderr, "[ksched pipe] cooperative launch too large: stream pipeline\n");
@@ -870,8 +873,8 @@ int enqueue_exact(ksched_ctx *c) {
     a.timeout_ticks = c->diag.exchange_timeout_ms * 100000;  // 100 MHz wall clock
     int e0 = -1;
     HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, c->stream));
-    HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, kExactBlock, G > 1,
-                           c->stream));
+    HIPCHK(c, launch_exact(npt, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, kExactBlock,
+                           G > 1 && !c->diag.plain_launch, c->stream));
     HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n, c->stream));
     c->st.pair_evals = c->p * n;
     c->st.batches = 0;
@@ -922,6 +925,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
     c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
+    c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 2);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);

@@ -499,8 +499,12 @@ constexpr size_t xchg_ring_bytes(int R, int B, int K) { return (size_t)4 * R * B
 // all ranks meet on the device and agree on the minimum of a small value (tag: this call's epoch0)
 hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hipStream_t s);
 // trace columns: score start (WG 0 past its wait), last arrival, last merge done, commit start, commit end
-constexpr int kTraceCols = 22;  // 0-15 stamps (col 13: exact rows), 16 the commit's counters, 17 its rescue waits,
-                                // 18-21 its prologue / guess / evaluate / check cycles (KSCHED_COMMIT_STAMPS)
+// trace row: 0-15 stamps (col 13: exact rows), 16 the commit's counters, 17 its rescue waits; with
+// KSCHED_COMMIT_STAMPS 18-21 its prologue / guess / evaluate / check cycles, 22-23 prologue marks (lists hashed, all
+// waves past), 24 before the wait, 25 entry -> past the wait, 26-30 the check step's split (update, probe, commit,
+// rescan, state load), 31-32 the guess step's (set-up, fixpoint), 33-36 the wave-0 state's (26-36: builds with
+// KSCHED_COMMIT_SPLIT only)
+constexpr int kTraceCols = 37;
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }

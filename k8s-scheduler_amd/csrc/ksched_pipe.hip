@@ -1266,6 +1266,10 @@ hipError_t pipe_one(const PipeLaunch &L0, int launch, PipeInfo *info, hipStream_
     }
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    if (launch == 2) {  // KSCHED_PLAIN_LAUNCH (profiled runs): the caller checked the occupancy
+        hipLaunchKernelGGL(fn, dim3(L.base[L.R]), dim3(kPipeThreads), lds, s, L);
+        return hipGetLastError();
+    }
     void *args[] = {&L};
     return hipLaunchCooperativeKernel((const void *)fn, dim3(L.base[L.R]), dim3(kPipeThreads), args, (unsigned)lds, s);
 }

@@ -8,6 +8,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 export TMPDIR=/tmp
+# the cooperative launch's runtime state faults in the HIP runtime's exit handler after rocprofv3's finalization
+# (DESIGN.md section 6.1): profiled runs launch the same kernels plainly, after the same occupancy check
+export KSCHED_PLAIN_LAUNCH=1
 tag=$1; shift
 out=gpurun_out/pmc_$tag
 mkdir -p "$out"

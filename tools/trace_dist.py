@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-COLS = 22
+COLS = 37
 
 
 def main():
@@ -64,13 +64,24 @@ def main():
         if s.any():
             print(f"  {r} rescues: {s.sum()} batches, commit mean {cm[s].mean():.1f} p50 {np.median(cm[s]):.1f} max {cm[s].max():.1f} us,"
                   f" rounds mean {rounds[s].mean():.2f}, resolved {done[s].mean():.1f}")
+    one = (cc & 0xffff) == 1
+    if one.any():
+        q = [t[b[one], c].mean() / 1e3 for c in (24, 25, 22, 23, 18)]
+        print(f"single-round batches, kcycles: before the wait {q[0]:.1f}, entry -> past the wait {q[1]:.1f}; after the wait:"
+              f" lists in + hashed {q[2]:.1f}, all waves past {q[3]:.1f}, prologue end {q[4]:.1f}")
+    if one.any():
+        q = [t[b[one], c].mean() / 1e3 for c in (33, 34, 35, 36)]
+        print(f"  wave-0 state, kcycles: fcc (list loads) {q[0]:.1f}, cut + list lengths {q[1]:.1f}, partial bests {q[2]:.1f},"
+              f" older export's best {q[3]:.1f}")
     print("commit time by rounds (kcycles per batch: prologue / guess / evaluate / check):")
     for lo, hi in ((0, 1), (1, 2), (2, 3), (3, 5), (5, 10), (10, 1 << 16)):
         s = (rounds >= lo) & (rounds < hi)
         if s.any():
-            kc = [t[b[s], c].mean() / 1e3 for c in (18, 19, 20, 21)]
+            kc = [t[b[s], c].mean() / 1e3 for c in (18, 19, 20, 21, 26, 27, 28, 29, 30, 31, 32)]
             print(f"  rounds [{lo},{hi}): {s.sum()} batches, commit mean {cm[s].mean():.1f} max {cm[s].max():.1f} us, total"
-                  f" {cm[s].sum() / 1e3:.2f} ms | {kc[0]:.1f} / {kc[1]:.1f} / {kc[2]:.1f} / {kc[3]:.1f}")
+                  f" {cm[s].sum() / 1e3:.2f} ms | {kc[0]:.1f} / {kc[1]:.1f} / {kc[2]:.1f} / {kc[3]:.1f}"
+                  f" (guess: set-up {kc[9]:.1f} fixpoint {kc[10]:.1f}; check: update {kc[4]:.1f} probe {kc[5]:.1f}"
+                  f" commit {kc[6]:.1f} [state load {kc[8]:.1f}] rescan {kc[7]:.1f})")
     # which phase of the chain is the long one when the period is long
     chain = us((t[b, 4] - t[b - lag, 4]).astype(np.float64))
     print(f"chain (commit(b-L) end -> commit(b) end): mean {chain.mean():.1f} p50 {np.median(chain):.1f} us = "
