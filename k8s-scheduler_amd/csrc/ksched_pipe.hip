@@ -920,15 +920,20 @@ __device__ __forceinline__ void inherit_x2_keys(const PersistArgs &P, int64_t b,
             k = kk;
             ix = x.idx;
         }
-        st_coh_f64(keys + lane, k);
     }
+    // pairs of keys as 16-byte sc1 stores (entries >= n2 are never read)
+    const double kn = __shfl_down(k, 1);
+    if (lane < n2 && (lane & 1) == 0)
+        st_coh16(coh_rsrc(keys), (uint32_t)(8 * lane),
+                 u32x4{(uint32_t)__double_as_longlong(k), (uint32_t)((uint64_t)__double_as_longlong(k) >> 32),
+                       (uint32_t)__double_as_longlong(kn), (uint32_t)((uint64_t)__double_as_longlong(kn) >> 32)});
     d = wave_sum_i64(d);
     int32_t src = lane;
     wave_argbest(k, ix, src);
     if (lane == 0) {
         uint64_t *sm = reinterpret_cast<uint64_t *>(P.inh + ((size_t)(b % 4) * P.B + m) * 32);
-        st_coh(sm, (uint64_t)d);
-        st_coh(sm + 1, (uint64_t)__double_as_longlong(k));
+        const uint64_t kb = (uint64_t)__double_as_longlong(k);
+        st_coh16(coh_rsrc(sm), 0, u32x4{(uint32_t)(uint64_t)d, (uint32_t)((uint64_t)d >> 32), (uint32_t)kb, (uint32_t)(kb >> 32)});
         st_coh(sm + 2, (uint64_t)(uint32_t)ix | (uint64_t)(uint32_t)(ix == kNoIdx ? -1 : src) << 32);
     }
 }
@@ -1021,8 +1026,21 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         ma.out_fc = reinterpret_cast<int64_t *>(lb + (size_t)P.B * K * sizeof(Rec));
         for (int m = g; m < P.B; m += kMS * P.M) {
             const bool xchg = P.R > 1 && p0 + m < NP;  // uniform over the merge waves
-            ma.lds_msg = xchg ? s_msg : nullptr;
+            // the pod's list is staged in LDS (the message the exchange sends, or the commit's list), so that it
+            // leaves as 16-byte sc1 stores (an 8-byte sc1 store costs a whole memory write request)
+            ma.lds_msg = p0 + m < NP ? s_msg : nullptr;
             merge_pod_fast<KC, K, true, kMT>(ma, m, mtid, ms, sync);
+            if (!xchg && p0 + m < NP) {
+                static_assert(K * sizeof(Rec) % 16 == 0, "a list is whole 16-byte chunks");
+                constexpr int kChunks = K * (int)sizeof(Rec) / 16;
+                sync();
+                if (mtid < kChunks) {
+                    const uint32_t *w = s_msg + 4 * mtid;
+                    st_coh16(coh_rsrc(ma.out_rec + (size_t)m * K), (uint32_t)(16 * mtid), u32x4{w[0], w[1], w[2], w[3]});
+                }
+                if (mtid == kChunks)
+                    st_coh(ma.out_fc + m, (uint64_t)s_msg[K * kRecWords] | (uint64_t)s_msg[K * kRecWords + 1] << 32);
+            }
             if (xchg) {
                 // this rank's list of pod m -> slot (a % 4, rank, m) of every rank's ring; then the R lists of
                 // pod m from this rank's ring -> rank merge -> the commit's list (lring)
