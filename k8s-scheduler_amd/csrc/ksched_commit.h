@@ -229,12 +229,27 @@ __device__ __forceinline__ LanePods load_lane_pods(const PodArgs &pods, int64_t 
 struct NoWait {
     __device__ bool operator()() const { return true; }
 };
+// The persistent pipeline's hand-off from commit(b - 1) (the other commit workgroup) to commit(b): called by every
+// thread; waits until commit(b - 1) has published, then returns what it left (0), the end of the call (1) or a
+// timeout (-1).  The stream pipeline's single commit kernel needs none.
+struct HandoffRes {
+    int64_t cursor;     // first unresolved pod after commit(b - 1)
+    int64_t plan_next;  // the plan of batch b + kPipeLag - 1, set by commit(b - 1)
+    int64_t rseq;       // rescue requests issued so far in the call
+    int32_t n1;         // entries of export(b - 1)
+    int32_t pad;
+};
+struct NoHandoff {
+    __device__ int operator()(HandoffRes *) const { return 0; }
+};
 
 // wait(): called by every thread once the work that needs no candidate list is done (the persistent
 // commit waits there for the batch's merges); false = give up (the caller reports the timeout).
-template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH, int NT = kSpcThreads, typename Wait = NoWait>
-__device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr,
-                                                 Wait wait = Wait{}) {
+// Returns 1 done, 0 error (a wait timed out), 2 the call ended elsewhere (persistent pipeline: stop quietly).
+template <int K, int PRIO, int DOM, bool LAB, bool F53, bool COH, int NT = kSpcThreads, typename Wait = NoWait,
+          typename Handoff = NoHandoff>
+__device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem, const LanePods *pre = nullptr,
+                                                Wait wait = Wait{}, Handoff handoff = Handoff{}) {
     constexpr int kSpcWaves = NT / 64;
     constexpr int kSpcThreads = NT;
     constexpr bool LAG3 = COH;  // the persistent pipeline runs at lag kPipeLag = 3
@@ -245,29 +260,42 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     const int wave = tid >> 6;
     PersistLocal *const L = A.loc;
     const int64_t p0 = COH ? L->plan[A.batch % kPlanRing] : load_i64<COH>(A.plan);
-    const int64_t cursor = COH ? L->cursor : load_i64<COH>(&A.ctl->cursor);
-    if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
-        if (!wait()) return false;
-        // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
-        if (wave == 0) {
-            if (lane == 0) {
-                if (COH) {
-                    // an empty export is never written: the slot keeps an older batch's tag, which score(b + 3)
-                    // reads as empty.  (An idle commit -- plan -1 -- does not wait for any merge, so a store here
-                    // could land under a score workgroup still reading the slot's previous export: ADVICE r3.)
-                    L->xcount2 = L->xcount;
-                    L->xcount = 0;
-                    if (p0 >= 0 && p0 < A.pods.p) st_coh(&A.ctl->stats[3], (uint64_t)++L->stats[3]);
-                    persist_plan(A, false, cursor);
-                } else {
+    if constexpr (COH) {
+        if (p0 < 0 || p0 >= A.pods.p) {
+            // nothing planned: after commit(b - 1), plan batch b + kPipeLag and publish.  An empty export is never
+            // written: the ring slot keeps an older batch's tag, which score(b + 3) and the commits read as empty.
+            // (An idle commit waits for no merge, so a store here could land under a score workgroup still
+            // reading the slot's previous export: ADVICE r3.)
+            if (!wait()) return 0;
+            HandoffRes ho;
+            const int hr = handoff(&ho);
+            if (hr != 0) return hr < 0 ? 0 : 2;
+            if (wave == 0) {
+                if (lane == 0) {
+                    L->cursor = ho.cursor;
+                    L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;
+                    L->rseq = ho.rseq;
+                    persist_plan(A, false, ho.cursor);
+                }
+                publish_committed<COH>(A);
+            }
+            return 1;
+        }
+    } else {
+        const int64_t cursor = load_i64<COH>(&A.ctl->cursor);
+        if (p0 < 0 || p0 >= A.pods.p || p0 != cursor) {
+            if (!wait()) return 0;
+            // nothing to do, or a speculative batch invalidated by an earlier truncation: skip it
+            if (wave == 0) {
+                if (lane == 0) {
                     A.xout->count = 0;
                     if (p0 >= 0 && p0 < A.pods.p) add_i64<COH>(&A.ctl->stats[3], 1);
                     plan_after_commit<COH>(A, false, cursor);
                 }
+                publish_committed<COH>(A);
             }
-            publish_committed<COH>(A);
+            return 1;
         }
-        return true;
     }
     const bool dbg = A.dbg != nullptr;  // diagnostics build of the phase timing (KSCHED_COMMIT_STAMPS)
     uint64_t t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
@@ -332,82 +360,26 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     };
     if constexpr (!COH) load_lists();
 
-    // ---- prologue part 1 (all waves; no candidate list needed): tables, inherited slots ----
-    // The inherited exports are loaded first, so their latency overlaps the table initialisation: wave 0
-    // lane e = entry e of the previous batch's export, wave 1 (lag 3) lane e = entry e of the one before it.
-    const int n1 = COH ? L->xcount : A.xin->count;  // <= 64 each
-    const int n2 = LAG3 ? L->xcount2 : 0;
-    XRec xi{};
-    if (wave == 0 && lane < n1) xi = load_xrec<COH>(A.xin->e, lane);
-    if (LAG3 && wave == 1 && lane < n2) xi = load_xrec<COH>(A.xin2->e, lane);
-    for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
-    if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
-    __syncthreads();
-    // slots [0, n1): the previous batch's commits; s0 = its start state (= this batch's snapshot at lag 2,
-    // and at lag 3 unless the node is also in the older export, which then overrides it below)
-    if (wave == 0 && lane < n1) {
-        SpcSlot &x = m.T[lane];
-        x.idx = xi.idx; x.mine = 0;
-        for (int r = 0; r < 3; ++r) { m.s0[lane * 3 + r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
-        x.labels = xi.labels; x.price = xi.price; x.pad = 0;
-        m.ti[lane] = xi.idx;
-        stage_state(m.iy + lane * 6, xi.cur);
-        const int h = spc_pos_insert(m.hk, xi.idx);
-        atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
-    }
-    int nin = n1;
-    if constexpr (LAG3) {
-        // slots [n1, nin): nodes only the batch before the previous one committed (a node both committed keeps
-        // the previous batch's slot).  Their keys and predicate deltas come from the merger workgroups, which
-        // computed them for every entry of that export while this batch merged (inherit_x2_keys,
-        // ksched_pipe.hip): the predicate deltas of the two exports add up (an entry's start state in the newer
-        // export is its state after the older one), so the older export's duplicates need no correction here.
-        __syncthreads();
-        if (wave == 1) {
-            bool fresh = false;
-            int h = 0;
-            if (lane < n2) {
-                bool existed;
-                h = spc_pos_insert(m.hk, xi.idx, &existed);
-                fresh = !existed;
-            }
-            const uint64_t fm = __ballot(fresh);
-            const int e = n1 + __popcll(fm & ((1ull << lane) - 1ull));
-            m.x2s[lane] = (lane < n2 && fresh) ? (int16_t)e : (int16_t)-1;
-            if (lane < n2 && fresh) {
-                SpcSlot &x = m.T[e];
-                x.idx = xi.idx; x.mine = 0;
-                for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
-                x.labels = xi.labels; x.price = xi.price; x.pad = 0;
-                m.ti[e] = xi.idx;
-                atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
-            }
-            if (lane == 0) m.ctl[3] = n1 + __popcll(fm);
-        }
-        __syncthreads();
-        nin = m.ctl[3];
-    } else {
-        __syncthreads();
-    }
-    // the slots whose keys this workgroup computes: all inherited slots at lag 2, the newer export's at lag 3
-    const int nkey = LAG3 ? n1 : nin;
-
+    // ---- prologue ----
+    int n1 = 0, n2 = 0, nin = 0;
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
     double *Srow = m.S + (size_t)lane * kSpcRow;
-
-    // inherited slots: keys at the current state, predicate deltas, per-wave partial row bests
-    {
+    uint64_t smv[3] = {0, 0, 0};  // COH: the merger's summary of this pod against the older export (wave 0)
+    // keys of the newer inherited export's entries at their current state, predicate deltas against the entry's
+    // start state s0, per-wave partial row bests; entry e -> slot sl(e)
+    auto key_inherited = [&](int ne, auto sl) {
         int dfl = 0;
         double pk = -__builtin_inf();
         int32_t pi = kNoIdx, ps = -1;
-        for (int t = wave; t < nkey; t += kSpcWaves) {
+        for (int e = wave; e < ne; e += kSpcWaves) {
+            const int t = sl(e);
             const SpcSlot &x = m.T[t];
-            const int64_t *x0 = m.s0 + t * 3;
+            const int64_t *x0 = m.s0 + e * 3;
             const bool f0 = fits(rc, rm, rp, sel, x0[0], x0[1], x0[2], x.labels, LAB);
             const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
             dfl += (int)f1 - (int)f0;
-            const double *yy = m.iy + t * 6;  // the slot's state as doubles and its reciprocals, staged once
+            const double *yy = m.iy + e * 6;  // the entry's state as doubles and its reciprocals, staged once
             double k;
             const bool el = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
                                                           yy[0], yy[1], yy[2], yy[3], yy[4], yy[5], y3, x.price, &k);
@@ -419,59 +391,160 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         m.pbk[wave * 64 + lane] = pk;
         m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
         if (dfl != 0) atomicAdd(&m.dfacc[lane], dfl);
-    }
-
-    // ---- prologue part 2: the candidate lists (hash positions of their entries) ----
-    if (dbg) {
-        t_pre = __builtin_amdgcn_s_memtime() - t_start;
-        if (COH && lane == 0 && wave != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[9]), (unsigned long long)t_pre);
-    }
-    if (!wait()) return false;  // a workgroup barrier when it waits
-    if (dbg) {
-        const uint64_t t = __builtin_amdgcn_s_memtime();
-        if (COH && tid == 0) A.dbg[7] += t - t_start;  // entry -> past the wait (wave 0)
-        t_start = t;
-    }
-    if constexpr (COH) load_lists();
-    // the merger's key columns of the older export's slots (LAG3, batch >= 2): element (pod j, entry e) of
-    // inh keys[batch % 4] into S[j][slot of e], loaded while the list entries are in flight
-    constexpr int kX2Per = 64 * 64 / kSpcThreads + (64 * 64 % kSpcThreads != 0);
-    double x2v[LAG3 ? kX2Per : 1];
-    const bool x2on = LAG3 && A.batch >= 2 && n2 > 0;
-    const double *x2col = LAG3 ? reinterpret_cast<const double *>(A.inh + (size_t)4 * A.B * 32) +
-                                     (size_t)(A.batch % 4) * A.B * 64
-                               : nullptr;
-    if constexpr (LAG3) {
+    };
+    // the batch's candidate lists -> LK / LI and their table positions HP
+    auto hash_lists = [&]() {
 #pragma unroll
-        for (int u = 0; u < kX2Per; ++u) {
-            const int i = tid + u * kSpcThreads;
-            x2v[u] = (x2on && i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) ? ld_coh_f64(x2col + i) : 0.0;
-        }
-    }
-#pragma unroll
-    for (int u = 0; u < kHeadPer; ++u) {
-        const int e = tid + u * kSpcThreads;
-        if (e < 64 * K) {
-            const int j = e / K, q = e % K;
-            const bool v = (uint32_t)(w1[u] >> 32) != 0;
-            const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
-            const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
-            m.LK[q * 64 + j] = key;
-            m.LI[q * 64 + j] = idx;
-            m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
-        }
-    }
-    if constexpr (LAG3) {
-#pragma unroll
-        for (int u = 0; u < kX2Per; ++u) {
-            const int i = tid + u * kSpcThreads;
-            if (x2on && i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) {
-                const int sl = m.x2s[i & 63];
-                if (sl >= 0) m.S[(size_t)(i >> 6) * kSpcRow + sl] = x2v[u];
+        for (int u = 0; u < kHeadPer; ++u) {
+            const int e = tid + u * kSpcThreads;
+            if (e < 64 * K) {
+                const int j = e / K, q = e % K;
+                const bool v = (uint32_t)(w1[u] >> 32) != 0;
+                const double key = v ? __longlong_as_double((long long)w0[u]) : -__builtin_inf();
+                const int32_t idx = v ? (int32_t)(uint32_t)w1[u] : kNoIdx;
+                m.LK[q * 64 + j] = key;
+                m.LI[q * 64 + j] = idx;
+                m.HP[q * 64 + j] = idx == kNoIdx ? kSpcInvalid : spc_pos_insert(m.hk, idx);
             }
         }
+    };
+    if constexpr (!COH) {
+        // ---- the stream pipeline (lag 2): slots [0, n1) = the previous batch's commits, s0 = their start state
+        // (= this batch's snapshot) ----
+        n1 = A.xin->count;  // <= 64
+        XRec xi{};
+        if (wave == 0 && lane < n1) xi = load_xrec<COH>(A.xin->e, lane);
+        for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
+        if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
+        __syncthreads();
+        if (wave == 0 && lane < n1) {
+            SpcSlot &x = m.T[lane];
+            x.idx = xi.idx; x.mine = 0;
+            for (int r = 0; r < 3; ++r) { m.s0[lane * 3 + r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+            x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+            m.ti[lane] = xi.idx;
+            stage_state(m.iy + lane * 6, xi.cur);
+            const int h = spc_pos_insert(m.hk, xi.idx);
+            atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
+        }
+        nin = n1;
+        __syncthreads();
+        key_inherited(n1, [](int e) { return e; });
+        if (!wait()) return 0;
+        hash_lists();
+        __syncthreads();
+    } else {
+        // ---- the persistent pipeline (lag 3; two commit workgroups alternate batches).  P1, while the other
+        // workgroup commits batch b - 1: the tables, the slots of export(b - 2) -- this workgroup's own previous
+        // batch --, the batch's lists and the mergers' keys of export(b - 2).  Then the hand-off from commit(b - 1)
+        // and P2: export(b - 1)'s slots and keys ----
+        {
+            const uint64_t hdr = A.batch >= 2 ? ld_coh(&A.xin2->count) : 0ull;
+            n2 = (A.batch >= 2 && (uint32_t)(hdr >> 32) == (uint32_t)(A.batch - 2)) ? (int)(uint32_t)hdr : 0;
+        }
+        XRec xi{};
+        if (wave == 1 && lane < n2) xi = load_xrec<COH>(A.xin2->e, lane);
+        for (int w = tid; w < kSpcHash; w += kSpcThreads) m.hk[w] = -1;
+        if (tid < 64) { m.dfacc[tid] = 0; m.fcg[tid] = 0; m.tkc[tid] = tid == (kSpcInvalid >> 5) ? (1u << (kSpcInvalid & 31)) : 0u; }
+        __syncthreads();
+        // slots [0, n2) = export(b - 2) in entry order (a node export(b - 1) also holds is superseded in P2); own[]
+        // (free until the guess step) maps their table positions to their slots
+        if (wave == 1) {
+            m.x2s[lane] = lane < n2 ? (int16_t)lane : (int16_t)-1;
+            if (lane < n2) {
+                SpcSlot &x = m.T[lane];
+                x.idx = xi.idx; x.mine = 0;
+                for (int r = 0; r < 3; ++r) { x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+                x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+                m.ti[lane] = xi.idx;
+                const int h = spc_pos_insert(m.hk, xi.idx);
+                m.own[h] = lane;
+                atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
+            }
+        }
+        if (dbg) {
+            t_pre = __builtin_amdgcn_s_memtime() - t_start;
+            if (lane == 0 && wave != 0) atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[9]), (unsigned long long)t_pre);
+        }
+        if (!wait()) return 0;  // the batch's merges (a workgroup barrier)
+        if (dbg) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (tid == 0) A.dbg[7] += t - t_start;  // entry -> past the merges' wait (wave 0)
+            t_start = t;
+        }
+        load_lists();
+        if (wave == 0 && A.batch >= 2 && n2 > 0 && pj) {
+            const uint64_t *sm = reinterpret_cast<const uint64_t *>(A.inh + ((size_t)(A.batch % 4) * A.B + lane) * 32);
+            smv[0] = ld_coh(sm); smv[1] = ld_coh(sm + 1); smv[2] = ld_coh(sm + 2);
+        }
+        // the mergers' key columns of export(b - 2): element (pod j, entry e) of inh keys[batch % 4] -> S[j][e]
+        constexpr int kX2Per = 64 * 64 / kSpcThreads + (64 * 64 % kSpcThreads != 0);
+        double x2v[kX2Per];
+        const double *x2col = reinterpret_cast<const double *>(A.inh + (size_t)4 * A.B * 32) + (size_t)(A.batch % 4) * A.B * 64;
+#pragma unroll
+        for (int u = 0; u < kX2Per; ++u) {
+            const int i = tid + u * kSpcThreads;
+            x2v[u] = (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) ? ld_coh_f64(x2col + i) : 0.0;
+        }
+        hash_lists();
+#pragma unroll
+        for (int u = 0; u < kX2Per; ++u) {
+            const int i = tid + u * kSpcThreads;
+            if (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) m.S[(size_t)(i >> 6) * kSpcRow + (i & 63)] = x2v[u];
+        }
+        // ---- the hand-off: commit(b - 1) published (a workgroup barrier) ----
+        HandoffRes ho;
+        const int hr = handoff(&ho);
+        if (hr != 0) return hr < 0 ? 0 : 2;  // timed out / the end of the call (or another workgroup's error)
+        if (tid == 0) {
+            L->cursor = ho.cursor;
+            L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;  // set by commit(b - 1)
+            L->rseq = ho.rseq;
+        }
+        if (p0 != ho.cursor) {  // speculative batch invalidated by a truncation in commit(b - 1): skip it
+            if (wave == 0) {
+                if (lane == 0) {
+                    __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&A.ctl->stats[3]), 1ull,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    persist_plan(A, false, ho.cursor);
+                }
+                publish_committed<COH>(A);
+            }
+            return 1;
+        }
+        n1 = ho.n1;
+        if (wave == 0 && lane < n1) xi = load_xrec<COH>(A.xin->e, lane);
+        // P2: export(b - 1).  A node export(b - 2) holds too keeps that slot (its state and key superseded: x2s = -1);
+        // the others take slots [n2, nin)
+        if (wave == 0) {
+            int h = 0;
+            bool dup = false;
+            if (lane < n1) {
+                h = spc_pos_insert(m.hk, xi.idx);
+                dup = (m.tkc[h >> 5] >> (h & 31)) & 1u;  // only export(b - 2)'s slots are taken yet
+            }
+            const uint64_t nm = __ballot(lane < n1 && !dup);
+            const int slot = dup ? m.own[h] : n2 + __popcll(nm & ((1ull << lane) - 1ull));
+            if (lane < n1) {
+                SpcSlot &x = m.T[slot];
+                x.idx = xi.idx; x.mine = 0;
+                for (int r = 0; r < 3; ++r) { m.s0[lane * 3 + r] = xi.sb[r]; x.sb[r] = xi.cur[r]; x.cur[r] = xi.cur[r]; }
+                x.labels = xi.labels; x.price = xi.price; x.pad = 0;
+                m.ti[slot] = xi.idx;
+                m.gs[lane] = slot;  // (gs is the guess step's; free until then)
+                stage_state(m.iy + lane * 6, xi.cur);
+                if (dup) m.x2s[slot] = -1;
+                else atomicOr(&m.tkc[h >> 5], 1u << (h & 31));
+            }
+            if (lane == 0) m.ctl[3] = n2 + __popcll(nm);
+        }
+        __syncthreads();
+        if (tid == 0 && A.trace_row) A.trace_row[23] = wall_clock64();  // export(b - 1) in its slots
+        nin = m.ctl[3];
+        key_inherited(n1, [&](int e) { return (int)m.gs[e]; });
+        __syncthreads();
+        if (tid == 0 && A.trace_row) A.trace_row[24] = wall_clock64();  // its keys
     }
-    __syncthreads();
 
     // ---- wave 0 state: lane j = pod j ----
     int32_t fcc = 0;          // predicate count with the confirmed commits
@@ -489,12 +562,10 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
         double xk = -__builtin_inf();
         int32_t xix = kNoIdx, xe = -1;
         if (LAG3 && A.batch >= 2 && n2 > 0 && pj) {  // the merger's summary: {sum of deltas, best key, idx | entry}
-            const uint64_t *sm = reinterpret_cast<const uint64_t *>(A.inh + ((size_t)(A.batch % 4) * A.B + lane) * 32);
-            ds2 = (int64_t)ld_coh(sm);
-            const uint64_t w2 = ld_coh(sm + 2);
-            xk = __longlong_as_double((long long)ld_coh(sm + 1));
-            xix = (int32_t)(uint32_t)w2;
-            xe = (int32_t)(w2 >> 32);
+            ds2 = (int64_t)smv[0];
+            xk = __longlong_as_double((long long)smv[1]);
+            xix = (int32_t)(uint32_t)smv[2];
+            xe = (int32_t)(smv[2] >> 32);
         }
         fcc = pj ? (int32_t)(fc0v + m.dfacc[lane] + ds2) : 0;
         cut = cut0;
@@ -510,8 +581,8 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
             if (m.x2s[xe] >= 0) {  // the best entry has a slot of its own
                 if (better(xk, xix, rbk, rbi)) { rbk = xk; rbi = xix; rbs = m.x2s[xe]; }
             } else {
-                // (rare) its node is also in the newer export, whose current state supersedes this key: the best
-                // of the entries that do have a slot, from the merger's key column
+                // its node is also in the newer export, whose current state superseded this key: the best of the
+                // entries that keep a slot of their own, from the mergers' key column
                 for (int e = 0; e < n2; ++e) {
                     if (m.x2s[e] < 0) continue;
                     const double k = Srow[m.x2s[e]];
@@ -524,6 +595,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     }
 
     int c = 0;
+    if (COH && tid == 0 && A.trace_row) A.trace_row[25] = wall_clock64();  // the rounds start
     const uint64_t t_pro = dbg ? __builtin_amdgcn_s_memtime() - t_start : 0;
     for (;;) {
         // ---- step 1 (wave 0): guesses for pods [c, cend) ----
@@ -898,12 +970,7 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     if (lane == 0) {
         if (COH) {
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
-            L->xcount2 = L->xcount;
-            L->xcount = base;
             L->cursor = p0 + done;
-            L->stats[0] += 1;
-            L->stats[1] += (done < nb) ? 1 : 0;
-            L->stats[2] += placed;
             persist_plan(A, done < nb, p0 + done);
         } else {
             A.xout->count = base;
@@ -928,14 +995,19 @@ __device__ __forceinline__ bool commit_spc_batch(const CommitArgs &A, char *smem
     if (COH) {
         // persistent pipeline: the outputs, the cursor and the counters are read by the host after the kernel
         // (and by the next call's commit), by no workgroup of this one -- off the hand-off's critical path
+        // (two commit workgroups: the counters are added, the cursor only grows)
         store_out();
         if (lane == 0) {
-            st_coh(&A.ctl->cursor, (uint64_t)L->cursor);
-            for (int i = 0; i < 3; ++i) st_coh(&A.ctl->stats[i], (uint64_t)L->stats[i]);
-            st_coh(&A.ctl->stats[4], (uint64_t)L->stats[4]);  // rescues
+            unsigned long long *st = reinterpret_cast<unsigned long long *>(A.ctl->stats);
+            __hip_atomic_fetch_max(reinterpret_cast<unsigned long long *>(&A.ctl->cursor), (unsigned long long)L->cursor,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(st + 0, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (done < nb) __hip_atomic_fetch_add(st + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(st + 2, (unsigned long long)placed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (nresc) __hip_atomic_fetch_add(st + 4, (unsigned long long)nresc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    return true;
+    return 1;
 }
 
 template <int K, int NT = kSpcThreads, bool LAG3 = false>

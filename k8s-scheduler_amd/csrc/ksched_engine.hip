@@ -684,9 +684,9 @@ int enqueue_persistent(ksched_ctx *c) {
     const int wgs = std::min(share, c->o.pipe_wgs > 0 ? c->o.pipe_wgs : c->cus);
     // merger workgroups: kPipeMergeSlots pods each, one slot per pod of a batch
     const int M = (B + kPipeMergeSlots - 1) / kPipeMergeSlots;
-    const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - 1 - M, (int64_t)kPipeMergeThreads,
+    const int G = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)wgs - kCommitWGs - M, (int64_t)kPipeMergeThreads,
                                                                (n_geom + 95) / 96}));
-    if (wgs < 2 + M) return 1;
+    if (wgs < kCommitWGs + 1 + M) return 1;
     const int R = (int)((n_geom + G - 1) / G);
     PipeLaunch L{};
     PersistArgs &a = L.P[0];
@@ -695,7 +695,7 @@ int enqueue_persistent(ksched_ctx *c) {
     a.M = M;
     a.B = B;
     L.R = 1;
-    L.base[1] = 1 + G + M;
+    L.base[1] = kCommitWGs + G + M;
     PipeInfo info{};
     const bool f53 = c->fast53, lab = c->o.use_labels != 0;
     hipError_t e = launch_pipe(KC, K, c->o.priority, c->o.domain, lab, f53, L, 0, &info, c->stream);
@@ -705,7 +705,7 @@ int enqueue_persistent(ksched_ctx *c) {
         fprintf(stderr, "[ksched pipe] G=%d rows/wg=%d LDS %zu+%zu B, %d VGPRs, %zu B scratch, %d WG/CU\n", G, R,
                 info.lds, info.static_lds, info.vgprs, info.spill, info.occ);
     if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
-    if (lgp && (info.occ < 1 || (int64_t)lgp->R * (1 + G + M) > (int64_t)(c->cus - kXcds) * info.occ))
+    if (lgp && (info.occ < 1 || (int64_t)lgp->R * (kCommitWGs + G + M) > (int64_t)(c->cus - kXcds) * info.occ))
         return fail(c, KSCHED_E_INVALID, "local rank group: the ranks' grids do not fit the device together");
     // workspace: part lists [kPipeLag][B][G][KC] with the counts in entry 0's pad (score(b + kPipeLag) reuses
     // batch b's), list ring 4 x (B*K Rec + B fc), XBuf ring
@@ -713,7 +713,7 @@ int enqueue_persistent(ksched_ctx *c) {
     const size_t cnt_b = 0;
     const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
     const size_t xb = align_up(xbuf_bytes(B), 256);
-    const size_t prog_b = align_up((size_t)(G + B + 1) * kProgWords * 8, 256);
+    const size_t prog_b = align_up((size_t)(G + B + kCommitWGs) * kProgWords * 8, 256);
     const size_t resc_b = align_up(rescue_bytes(B), 256);
     const size_t inh_b = align_up(inh_bytes(B), 256);
     const size_t need = part_b + cnt_b + 4 * lists_b + 5 * xb + prog_b + resc_b + inh_b;
@@ -780,7 +780,7 @@ int enqueue_persistent(ksched_ctx *c) {
     }
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
-    HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + 1) * kProgWords * 8, sS));
+    HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + kCommitWGs) * kProgWords * 8, sS));
     // timing: the kernel (family 0) is bracketed by events on its stream -- one launch per call, so the
     // events cost nothing per batch and may stay on inside a timed region
     int e0 = -1;
@@ -809,7 +809,7 @@ int enqueue_persistent(ksched_ctx *c) {
                 if (g->launch_err != hipSuccess) return;
                 g->L.R = g->R;
                 g->L.base[0] = 0;
-                for (int r = 0; r < g->R; ++r) g->L.base[r + 1] = g->L.base[r] + 1 + g->L.P[r].G + g->L.P[r].M;
+                for (int r = 0; r < g->R; ++r) g->L.base[r + 1] = g->L.base[r] + kCommitWGs + g->L.P[r].G + g->L.P[r].M;
                 hipError_t le = hipSuccess;
                 for (int r = 0; r < g->R && le == hipSuccess; ++r)
                     if (r != me) le = hipStreamWaitEvent(sS, g->ready[r], 0);
@@ -1493,7 +1493,7 @@ int ksched_run(ksched_ctx *c) {
 // with where it ran and whether a merger workgroup shared its CU (PersistArgs::prog words 2, 3).
 static void print_wg_busy(ksched_ctx *c) {
     if (!c->d_prog) return;
-    const int G = c->prog_G, B = c->prog_B, n = G + B + 1;
+    const int G = c->prog_G, B = c->prog_B, n = G + B + kCommitWGs;
     std::vector<uint64_t> w((size_t)kProgWords * n);
     if (hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     auto where = [&](int i) { return (uint32_t)(w[kProgWords * i + 1] >> 32); };
@@ -1528,7 +1528,7 @@ static void print_wg_busy(ksched_ctx *c) {
 // and what their last wait saw (PersistArgs::prog).
 static std::string progress_summary(ksched_ctx *c) {
     if (!c->d_prog) return "";
-    const int n = c->prog_G + c->prog_B + 1;
+    const int n = c->prog_G + c->prog_B + kCommitWGs;
     std::vector<uint64_t> w((size_t)kProgWords * n);
     if (hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return "";
     const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
@@ -1565,12 +1565,12 @@ static std::string progress_summary(ksched_ctx *c) {
     group("score", 0, c->prog_G);
     group("merge", c->prog_G, c->prog_G + c->prog_B);
     group("commit", c->prog_G + c->prog_B, n);
-    {
-        const int i = n - 1;
+    for (int i = c->prog_G + c->prog_B; i < n; ++i) {
         const uint32_t where = (uint32_t)(w[kProgWords * i + 1] >> 32);
-        char t[120];
-        snprintf(t, sizeof t, "; commit phase %#x on xcc %u se %u cu %u", (unsigned)(w[kProgWords * i] & 0xff),
-                 (where >> 8) & 0xf, (where >> 4) & 0xf, where & 0xf);
+        char t[160];
+        snprintf(t, sizeof t, "; commit workgroup %d: batch %lld phase %#x on xcc %u se %u cu %u", i - c->prog_G - c->prog_B,
+                 (long long)(w[kProgWords * i] >> 8), (unsigned)(w[kProgWords * i] & 0xff), (where >> 8) & 0xf,
+                 (where >> 4) & 0xf, where & 0xf);
         out += t;
     }
     return out;

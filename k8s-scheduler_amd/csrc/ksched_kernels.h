@@ -106,6 +106,8 @@ constexpr int kPlanRing = 8;
 // and commit(b) inherits the nodes the kPipeLag - 1 batches before it committed.
 // The stream pipeline runs at lag 2.
 constexpr int kPipeLag = 3;
+// The persistent pipeline's commit workgroups: they alternate batches (ksched_pipe.hip commit_role)
+constexpr int kCommitWGs = 2;
 constexpr int kCtlReplicas = 8;
 struct alignas(128) CtlLine {
     unsigned long long v;

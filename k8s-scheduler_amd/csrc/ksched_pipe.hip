@@ -1089,34 +1089,48 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
 }
 
 // ------------------------------------------------------------------------------------------------
-// COMMIT role (workgroup 0, all kPipeWaves = 12 waves): batch after batch, wait for the B merges of an active batch
-// (Ctl::merged), commit it (commit_spc_batch: lists read with sc1 loads; export, plans and cursor left as
-// sc1 stores), publish Ctl::committed.  Once every pod is resolved it publishes a committed count no wait
-// can exceed, so every workgroup still waiting sees the end.
+// COMMIT role (workgroups 0 and 1, all kPipeWaves = 12 waves each): workgroup `par` commits the batches
+// b = par, par + 2, ... .  Per batch: the work that does not depend on commit(b - 1) -- tables, the slots of
+// export(b - 2), the wait for the batch's B merges (Ctl::merged), its lists, the mergers' keys -- runs while the
+// other workgroup commits b - 1; then the hand-off (Ctl::committed >= b: commit(b - 1) published its cursor,
+// plans and export), the rest of the commit (commit_spc_batch), Ctl::committed = b + 1.  The plans, the cursor
+// and the export travel through global memory (sc1), so the two workgroups share no LDS state.  Once every pod
+// is resolved, the workgroup that resolved the last one publishes a committed count no wait can exceed, so
+// every workgroup still waiting -- the other commit workgroup included -- sees the end.
 // ------------------------------------------------------------------------------------------------
 template <int K, int PRIO, int DOM, bool LAB, bool F53>
-__device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
+__device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, const int par) {
     __builtin_amdgcn_s_setprio(3);
     PersistLocal &loc = *reinterpret_cast<PersistLocal *>(smem);
     char *cs = smem + commit_loc_bytes();
     __shared__ int s_stop;
+    __shared__ HandoffRes s_ho;
+    __shared__ int s_hr;
     Ctl *ctl = P.ctl;
-    // k_ctl_init ran before this kernel on the stream: take the initial plans / cursor / stats once
-    if (threadIdx.x < kPlanRing) loc.plan[threadIdx.x] = (int64_t)ld_rmw(&ctl->plan[threadIdx.x]);
+    // k_ctl_init ran before this kernel on the stream: the call's initial cursor
     if (threadIdx.x == 0) {
         loc.cursor = (int64_t)ld_rmw(&ctl->cursor);
-        for (int i = 0; i < 5; ++i) loc.stats[i] = (int64_t)ld_rmw(&ctl->stats[i]);
+        for (int i = 0; i < 5; ++i) loc.stats[i] = 0;
         loc.xcount = 0;
         loc.xcount2 = 0;
         loc.rseq = 0;
     }
     __syncthreads();
-    const int cslot = P.G + P.B;  // progress slot
-    int64_t nact = 0;
+    const int64_t cursor0 = loc.cursor;
+    const int cslot = P.G + P.B + par;  // progress slot
+    constexpr int kPoller = 128;  // wave 2 lane 0: its wave loads nothing else in the prologue
+    const int rep = (par + kCtlReplicas - 1) % kCtlReplicas;  // the committed replica this workgroup polls
+    int64_t nact = 0;  // active batches among 0 .. b (both workgroups' batches)
     int idle = 0;
-    for (int64_t b = 0;; ++b) {
-        const int64_t p0 = loc.plan[b % kPlanRing];  // written by this workgroup (or k_ctl_init)
-        if (!(p0 >= 0 && p0 < P.pods.p) && ++idle > kPlanRing) {
+    for (int64_t b = par;; b += 2) {
+        // the plans of b - 1 and b were set by commits b - 4 and b - 3 (or k_ctl_init), both published before
+        // this workgroup's commit(b - 2) finished
+        const int64_t p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+        const int64_t pm = b >= 1 ? (int64_t)ld_coh(&ctl->plan[(b - 1) % kPlanRing]) : -1;
+        const bool act = p0 >= 0 && p0 < P.pods.p;
+        nact += ((b >= 1 && pm >= 0 && pm < P.pods.p) ? 1 : 0) + (act ? 1 : 0);
+        if (threadIdx.x == 0) loc.plan[b % kPlanRing] = p0;
+        if (!act && ++idle > kPlanRing) {
             // pods remain but nothing is planned: a truncation re-plans within kPipeLag batches, so this is a
             // protocol error -- stop everyone instead of spinning
             if (threadIdx.x == 0) atomicCAS(P.err, 0, 9);
@@ -1125,14 +1139,11 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         }
         if (threadIdx.x == 0) trace_at(P, b, 15);
         LanePods pre{0, 0, 0, 0};
-        const bool act = p0 >= 0 && p0 < P.pods.p;
-        constexpr int kPoller = 128;  // wave 2 lane 0: its wave loads nothing else in the prologue
         unsigned long long early_m = 0;
         if (act) {
             idle = 0;
-            ++nact;
-            // the pods' requests are known now: their loads overlap the inherited-slot work
-            if (p0 == loc.cursor) pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
+            // the pods' requests: their loads overlap the prologue (a batch voided by commit(b - 1) discards them)
+            pre = load_lane_pods<LAB>(P.pods, p0, (int)(P.pods.p - p0 < P.B ? P.pods.p - p0 : P.B));
             // the merge count, read now: its latency hides behind the prologue (the merges are usually done)
             if (threadIdx.x == kPoller)
                 early_m = __hip_atomic_load(&ctl->merged[(nact - 1) % 4].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1161,6 +1172,37 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
             if (threadIdx.x == 0) trace_at(P, b, 3);
             return true;
         };
+        // commit(b - 1) -> commit(b): Ctl::committed >= b, then what commit(b - 1) stored before publishing it
+        auto handoff = [&](HandoffRes *r) -> int {
+            if (threadIdx.x == kPoller) {
+                int st = 0;
+                unsigned long long seen = b;
+                if (b > 0) {
+                    prog_at(P, cslot, b, kProgWaitCommit, 0);
+                    if (!poll_ge(&ctl->committed_x[rep].v, (unsigned long long)b, P.timeout_ticks, &ctl->polls_rmw, &seen)) {
+                        prog_at(P, cslot, b, kProgWaitCommit | kProgTimedOut, seen);
+                        st = -1;
+                    } else if (seen >= (1ull << 62)) {
+                        st = 1;  // the end of the call, or another workgroup's error
+                    }
+                }
+                HandoffRes h{};
+                if (st == 0) {
+                    h.cursor = b > 0 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 1) % kPlanRing]) : cursor0;
+                    h.plan_next = (int64_t)ld_coh(&ctl->plan[(b + kPipeLag - 1) % kPlanRing]);
+                    h.rseq = (int64_t)__hip_atomic_load(&ctl->rescue_req.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes);
+                    const uint64_t hdr = b >= 1 ? ld_coh(&xb->count) : 0ull;
+                    h.n1 = (b >= 1 && (uint32_t)(hdr >> 32) == (uint32_t)(b - 1)) ? (int32_t)(uint32_t)hdr : 0;
+                }
+                s_ho = h;
+                s_hr = st;
+            }
+            __syncthreads();
+            *r = s_ho;
+            if (threadIdx.x == 0) trace_at(P, b, 22);  // past the hand-off
+            return s_hr;
+        };
         CommitArgs ca{};
         char *lb = P.lring + (size_t)(b % 4) * P.lists_bytes;
         ca.lists = reinterpret_cast<const Rec *>(lb);
@@ -1185,7 +1227,9 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem) {
         ca.inh = P.inh;
         ca.timeout_ticks = P.timeout_ticks;
         ca.err = P.err;
-        if (!commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged)) {
+        const int rc = commit_spc_batch<K, PRIO, DOM, LAB, F53, true, kPipeThreads>(ca, cs, &pre, wait_merged, handoff);
+        if (rc == 2) return;  // the call ended (or failed) elsewhere
+        if (rc == 0) {
             if (threadIdx.x == 0) atomicCAS(P.err, 0, 5);
             if (threadIdx.x < 64) publish_committed_all(ctl, 1ull << 62);
             return;
@@ -1218,24 +1262,24 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
         for (int i = (int)threadIdx.x; i < P.poison_lds / 4; i += kPipeThreads) reinterpret_cast<uint32_t *>(smem)[i] = ~0u;
         __syncthreads();
     }
-    if (blk == 0) {
+    if (blk < kCommitWGs) {
 #ifndef KSCHED_PROBE_NO_COMMIT
-        commit_role<K, PRIO, DOM, LAB, F53>(P, smem);
+        commit_role<K, PRIO, DOM, LAB, F53>(P, smem, blk);
 #endif
         return;
     }
-    if (blk <= P.G) {
+    if (blk < kCommitWGs + P.G) {
         PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
         if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
         __syncthreads();
 #ifndef KSCHED_PROBE_NO_SCORE
-        score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, blk - 1);
+        score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, blk - kCommitWGs);
 #endif
         return;
     }
     // a merger workgroup: kMS independent pod slots of kMT threads
     const int slot = (int)threadIdx.x / kMT;
-    const int id = (blk - 1 - P.G) * kMS + slot;
+    const int id = (blk - kCommitWGs - P.G) * kMS + slot;
     char *sbase = smem + (size_t)slot * MergeLayout<KC, K>::slot_bytes;
     if (threadIdx.x % kMT == 0) reinterpret_cast<MergeCtl *>(sbase)->mbar = 0;
     __syncthreads();  // the only workgroup-wide barrier: before the slots part
@@ -1279,7 +1323,7 @@ hipError_t pipe_one(const PipeLaunch &L0, int launch, PipeInfo *info, hipStream_
     if (L.R < 1 || L.R > kMaxLocalRanks || L.base[0] != 0) return hipErrorInvalidValue;
     for (int r = 0; r < L.R; ++r) {
         const PersistArgs &a = L.P[r];
-        if (a.G > kMT || a.B > 64 || a.M * kMS < a.B || L.base[r + 1] - L.base[r] != 1 + a.G + a.M)
+        if (a.G > kMT || a.B > 64 || a.M * kMS < a.B || L.base[r + 1] - L.base[r] != kCommitWGs + a.G + a.M)
             return hipErrorInvalidValue;
     }
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

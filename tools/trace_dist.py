@@ -31,6 +31,15 @@ def main():
         "wg0 score busy (start -> its arrival)": t[b, 5] - t[b, 0],
         "loop top -> past wait": t[b, 3] - t[b, 15],
     }
+    if (t[b, 22] > 0).all():  # two commit workgroups: P1, the hand-off, the rest
+        ph["P1: past merges' wait -> past the hand-off"] = t[b, 22] - t[b, 3]
+        ph["commit(b-1) end -> past the hand-off"] = t[b, 22] - t[b - 1, 4]
+        ph["past the hand-off -> commit end"] = t[b, 4] - t[b, 22]
+        if (t[b, 25] > 0).all():
+            ph["  hand-off -> export(b-1) in slots"] = t[b, 23] - t[b, 22]
+            ph["  -> its keys"] = t[b, 24] - t[b, 23]
+            ph["  -> rounds start (wave-0 state)"] = t[b, 25] - t[b, 24]
+            ph["  rounds start -> commit end"] = t[b, 4] - t[b, 25]
     print(f"{len(b)} batches (lag {lag})")
     print(f"{'phase':48s} {'mean':>7s} {'p10':>7s} {'p50':>7s} {'p90':>7s} {'p99':>7s} {'max':>9s}  (us)")
     for k, v in ph.items():
