@@ -26,7 +26,8 @@ def test_persistent_timeout_reports_and_recovers(gpu_available, oracle_mod):
             e.sync()
         msg = str(ex.value)
         assert "persistent pipeline" in msg and "timed out" in msg, msg
-        assert "score batches" in msg and "commit phase" in msg, msg  # the progress words
+        # the progress words: the score workgroups' batches and both commit workgroups' batch and phase
+        assert "score batches" in msg and "commit workgroup 0" in msg and "commit workgroup 1" in msg, msg
         e.set_timeout(10000)
 
         def again():
