@@ -242,6 +242,13 @@ struct HandoffRes {
 struct NoHandoff {
     __device__ int operator()(HandoffRes *) const { return 0; }
 };
+// commit(b)'s hand-off record for commit(b + 1) (one lane; every store it describes already drained)
+__device__ __forceinline__ void put_handoff(Ctl *ctl, int64_t batch, int n1, int64_t cursor, int64_t rseq, int64_t plan_next) {
+    const __amdgpu_buffer_rsrc_t r = coh_rsrc(&ctl->hrec);
+    const uint32_t tag = (uint32_t)(batch + 1);
+    st_coh16(r, 0, u32x4{tag, (uint32_t)n1, (uint32_t)(uint64_t)cursor, (uint32_t)((uint64_t)cursor >> 32)});
+    st_coh16(r, 16, u32x4{tag, (uint32_t)rseq, (uint32_t)(uint64_t)plan_next, (uint32_t)((uint64_t)plan_next >> 32)});
+}
 
 // wait(): called by every thread once the work that needs no candidate list is done (the persistent
 // commit waits there for the batch's merges); false = give up (the caller reports the timeout).
@@ -276,6 +283,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;
                     L->rseq = ho.rseq;
                     persist_plan(A, false, ho.cursor);
+                    drain_stores();  // the plan before the record
+                    put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
             }
@@ -507,6 +516,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&A.ctl->stats[3]), 1ull,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     persist_plan(A, false, ho.cursor);
+                    drain_stores();  // the plan before the record
+                    put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
             }
@@ -972,6 +983,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
             L->cursor = p0 + done;
             persist_plan(A, done < nb, p0 + done);
+            drain_stores();  // the export and the plan before the record that announces them
+            put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
         } else {
             A.xout->count = base;
             store_i64<COH>(&A.ctl->cursor, p0 + done);

@@ -138,6 +138,10 @@ struct alignas(128) Ctl {
     // rescue_done (B per request)
     CtlLine rescue_req;
     CtlLine rescue_done;
+    // the persistent pipeline's hand-off between its two commit workgroups: commit(b) leaves two 16-byte sc1
+    // granules, each tagged b + 1: {tag, export count, cursor} and {tag, rescue requests, plan of b + 3}; commit(b + 1)
+    // polls them instead of Ctl::committed and a second round of loads
+    CtlLine hrec;
 };
 // The rescue request the commit writes (PersistArgs::rescue; sc1 stores, then Ctl::rescue_req) and the merger
 // slots' results after it: {rc, rm, rp, sel, nT} and the touched set's node indices, then Rec res[B].

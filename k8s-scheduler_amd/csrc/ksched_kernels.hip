@@ -847,6 +847,7 @@ __global__ void k_ctl_init(Ctl *ctl, int B, int64_t P, int lag) {
     for (int i = 0; i < kCtlReplicas; ++i) ctl->committed_x[i].v = 0;
     ctl->rescue_req.v = 0;
     ctl->rescue_done.v = 0;
+    for (int i = 0; i < 16; ++i) (&ctl->hrec.v)[i] = 0;  // (v and pad: the two hand-off granules)
     ctl->polls_rmw = 0;
     for (int i = 0; i < kPlanRing; ++i) ctl->cursor_at[i] = 0;
     ctl->nact = 0;

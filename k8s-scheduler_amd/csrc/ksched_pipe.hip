@@ -1172,28 +1172,40 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
             if (threadIdx.x == 0) trace_at(P, b, 3);
             return true;
         };
-        // commit(b - 1) -> commit(b): Ctl::committed >= b, then what commit(b - 1) stored before publishing it
+        // commit(b - 1) -> commit(b): the two hand-off granules tagged b (Ctl::hrec, put_handoff) -- or the end of
+        // the call (Ctl::committed >= 2^62: the last pod resolved, or an error elsewhere)
         auto handoff = [&](HandoffRes *r) -> int {
             if (threadIdx.x == kPoller) {
                 int st = 0;
-                unsigned long long seen = b;
-                if (b > 0) {
-                    prog_at(P, cslot, b, kProgWaitCommit, 0);
-                    if (!poll_ge(&ctl->committed_x[rep].v, (unsigned long long)b, P.timeout_ticks, &ctl->polls_rmw, &seen)) {
-                        prog_at(P, cslot, b, kProgWaitCommit | kProgTimedOut, seen);
-                        st = -1;
-                    } else if (seen >= (1ull << 62)) {
-                        st = 1;  // the end of the call, or another workgroup's error
-                    }
-                }
                 HandoffRes h{};
-                if (st == 0) {
-                    h.cursor = b > 0 ? (int64_t)ld_coh(&ctl->cursor_at[(b - 1) % kPlanRing]) : cursor0;
-                    h.plan_next = (int64_t)ld_coh(&ctl->plan[(b + kPipeLag - 1) % kPlanRing]);
-                    h.rseq = (int64_t)__hip_atomic_load(&ctl->rescue_req.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes);
-                    const uint64_t hdr = b >= 1 ? ld_coh(&xb->count) : 0ull;
-                    h.n1 = (b >= 1 && (uint32_t)(hdr >> 32) == (uint32_t)(b - 1)) ? (int32_t)(uint32_t)hdr : 0;
+                if (b == 0) {
+                    h.cursor = cursor0;
+                    h.plan_next = (int64_t)ld_coh(&ctl->plan[(kPipeLag - 1) % kPlanRing]);
+                } else {
+                    prog_at(P, cslot, b, kProgWaitCommit, 0);
+                    const __amdgpu_buffer_rsrc_t hr = coh_rsrc(&ctl->hrec);
+                    const uint64_t t0 = wall_clock64();
+                    for (int it = 1;; ++it) {
+                        const u32x4 c0 = ld_coh16(hr, 0), c1 = ld_coh16(hr, 16);
+                        if (c0.x == (uint32_t)b && c1.x == (uint32_t)b) {
+                            h.n1 = (int32_t)c0.y;
+                            h.cursor = (int64_t)((uint64_t)c0.w << 32 | c0.z);
+                            h.rseq = (int64_t)c1.y;
+                            h.plan_next = (int64_t)((uint64_t)c1.w << 32 | c1.z);
+                            break;
+                        }
+                        if ((it & 63) == 0) {
+                            const unsigned long long cm =
+                                __hip_atomic_load(&ctl->committed_x[rep].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (cm >= (1ull << 62)) { st = 1; break; }
+                            if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) {
+                                prog_at(P, cslot, b, kProgWaitCommit | kProgTimedOut, cm);
+                                st = -1;
+                                break;
+                            }
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
                 }
                 s_ho = h;
                 s_hr = st;
