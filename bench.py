@@ -28,7 +28,7 @@ FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-s
 # PMC summaries of the same workloads (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ
 # passes of `bench.py` itself); keyed by (kernel, config, batch, ranks)
 PMC_SUMMARIES = {
-    ("k_pipe", "c4", 64, 1): os.path.join(ROOT, "profiles", "r03_pmc_c4_pipe.json"),
+    ("k_pipe", "c4", 64, 1): os.path.join(ROOT, "profiles", "r04_pmc_c4_pipe.json"),
     ("k_score_topk", "c4", 64, 1): os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json"),
 }
 
@@ -43,8 +43,12 @@ def pmc_summary(kernel, config, batch, world):
         k = json.load(f)["kernels"].get(kernel)
     if not k or "fabric_bytes_per_launch" not in k:
         return None
+    with open(path) as f:
+        src_commit = json.load(f).get("source_commit")
     out = {"traffic": k["fabric_bytes_per_launch"], "traffic_source": os.path.relpath(path, ROOT),
-           "traffic_unit": "bytes per launch (FETCH_SIZE + WRITE_SIZE)"}
+           "traffic_unit": "bytes per launch (2 x FETCH_SIZE + WRITE_SIZE)"}
+    if src_commit:
+        out["traffic_source_commit"] = src_commit
     for f in ("hbm_gbs", "valu_busy_frac", "fp64_issue_frac", "active_inst_valu_frac"):
         if f in k:
             out[f"pmc_{f}"] = k[f]
