@@ -43,7 +43,8 @@ def run(spec, reps=2):
         oi, _, _ = e.results()
     out = dict(spec=spec, pods=cl.n_pods, nodes=cl.n_nodes, wall_s=dt, evals_per_s=cl.n_pods * cl.n_nodes / dt,
                pods_per_s=cl.n_pods / dt, placed=int((oi >= 0).sum()), batches=st["batches"],
-               truncations=st["truncations"], device_ms=st["device_ms"],
+               truncations=st["truncations"], rescues=st.get("rescues"), pipeline=st.get("pipeline"),
+               device_ms=st["device_ms"],
                fam_avg_ms=[st["kernel_ms"][f] / max(st["kernel_launches"][f], 1) for f in range(4)],
                fam_timed=st["kernel_launches"])
     print(json.dumps(out), flush=True)
