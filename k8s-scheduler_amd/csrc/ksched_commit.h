@@ -635,14 +635,15 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             int32_t pq = -1, ph = kSpcInvalid;  // current proposal (list position, table position)
             for (int it = 0;; ++it) {
                 ++niters;
+                // the first entry not confirmed-taken and not proposed by an earlier pod: every probe of own[] in
+                // flight at once (highest entry first, so the lowest match is the one kept), no branch per entry
                 int32_t nq = -1, nh = kSpcInvalid;
-                bool open = am != 0;  // still probing
+                if (am) {
 #pragma unroll
-                for (int qq = 0; qq < K; ++qq) {
-                    if (!__ballot(open)) break;  // uniform: every lane has its proposal
-                    if (open) {
-                        if (((am >> qq) & 1u) && m.own[hp[qq]] >= lane) { nq = qq; nh = hp[qq]; open = false; }
-                        else if ((am >> qq) <= 1u) open = false;  // no later candidate
+                    for (int qq = K - 1; qq >= 0; --qq) {
+                        const bool ok = (((am >> qq) & 1u) != 0u) & (m.own[hp[qq]] >= lane);
+                        nq = ok ? qq : nq;
+                        nh = ok ? hp[qq] : nh;
                     }
                 }
                 const bool changed = __ballot(act && nq != pq) != 0;
