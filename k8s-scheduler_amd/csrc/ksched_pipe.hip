@@ -1010,6 +1010,13 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         ++nact;
         const int slot = (int)((nact - 1) % 4);
         const unsigned long long use = (unsigned long long)((nact - 1) / 4);
+        // the pods' keys against the older inherited export, while the score workgroups still scan the batch
+        // (commit(b - 2) usually ends well before the batch's last arrival): off the merge -> commit path
+        if (P.inh && b >= 2) {
+            if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit)) return;
+            for (int m = g; m < P.B; m += kMS * P.M)
+                if (p0 + m < NP) inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid);
+        }
         if (!mwait(b, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, 7, kProgWaitArrive)) return;
         if (mtid == 0 && g == 0) trace_at(P, b, 7);
         const size_t part_elems = (size_t)P.B * G;
@@ -1068,12 +1075,6 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
                 sync();
                 if (pc->m_stop) return;
                 if (mtid < 64) rank_merge_msgs<K>(s_all, RR, ma.out_rec + (size_t)m * K, ma.out_fc + m);
-            }
-            // the pod's keys against the older inherited export (commit(b - 2) done: usually long since)
-            if (P.inh && b >= 2 && p0 + m < NP) {
-                if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit))
-                    return;
-                inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid);
             }
             drain_stores();
             sync();  // every merge wave's stores drained before the count; LDS free for the next pod
