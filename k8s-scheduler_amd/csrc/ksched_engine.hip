@@ -781,6 +781,8 @@ int enqueue_persistent(ksched_ctx *c) {
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
     for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
     HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + kCommitWGs) * kProgWords * 8, sS));
+    // score -> merge records carry 16-bit batch tags (1 + batch): no record of an earlier call may look current
+    HIPCHK(c, hipMemsetAsync(a.part, 0, part_b, sS));
     // timing: the kernel (family 0) is bracketed by events on its stream -- one launch per call, so the
     // events cost nothing per batch and may stay on inside a timed region
     int e0 = -1;

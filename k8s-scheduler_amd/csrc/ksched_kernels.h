@@ -220,6 +220,7 @@ struct MergeArgs {
     int64_t p0v;
     int32_t *err;                        // device error word
     uint32_t *lds_msg;                   // non-null: the final list goes to LDS as a PodMsg (kMsgWords)
+    uint32_t tag;                        // persistent pipeline: the batch's 16-bit record tag (score_role)
 };
 
 // One pod's merged candidate list as 32-bit words, the unit the ranks exchange in the persistent
@@ -510,7 +511,7 @@ hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hip
 // waves past), 24 before the wait, 25 entry -> past the wait, 26-30 the check step's split (update, probe, commit,
 // rescan, state load), 31-32 the guess step's (set-up, fixpoint), 33-36 the wave-0 state's (26-36: builds with
 // KSCHED_COMMIT_SPLIT only)
-constexpr int kTraceCols = 37;
+constexpr int kTraceCols = 49;  // + 37-48: score WG 0's waves' pass-1 ends
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }

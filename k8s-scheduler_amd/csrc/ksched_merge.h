@@ -313,6 +313,25 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         u32x4 w[KC];
 #pragma unroll
         for (int q = 0; q < KC; ++q) w[q] = ld_coh16(rs, off + (uint32_t)(q * sizeof(Cand)));
+        // every record carries its batch's tag (word 3, bits 16..31): a score workgroup arrives without draining
+        // its record stores, so a record may still be on its way -- read again until all KC are this batch's
+        if (has) {
+            auto stale = [&]() {
+                bool st = false;
+#pragma unroll
+                for (int q = 0; q < KC; ++q) st |= (w[q].w >> 16) != A.tag;
+                return st;
+            };
+            for (int it = 0; stale(); ++it) {
+                if (it == (1 << 22)) {  // (never seen: a lost store) -- report, do not hang
+                    if (A.err) atomicCAS(A.err, 0, 11);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+                for (int q = 0; q < KC; ++q) w[q] = ld_coh16(rs, off + (uint32_t)(q * sizeof(Cand)));
+            }
+        }
 #pragma unroll
         for (int q = 0; q < KC; ++q) {
             const int32_t x = has ? (int32_t)w[q].z : kNoIdx;
@@ -321,7 +340,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
             code[q] = x == kNoIdx ? 0ull : key_code(kq);
             n += x != kNoIdx;
         }
-        cnt = has ? (int64_t)(int32_t)w[0].w : 0;
+        cnt = has ? (int64_t)(w[0].w & 0xffffu) : 0;
     }
 #pragma unroll
     for (int q = 0; q < KC; ++q) { sm.code[tid][q] = code[q]; sm.idx[tid][q] = idx[q]; }

@@ -738,11 +738,16 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 ii = src == q ? idx[q] : ii;
             }
             const uint64_t kb = (uint64_t)__double_as_longlong(kk);
-            const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, src == 0 ? (uint32_t)s_cnt[pl] : 0u};
+            // word 3: the batch's tag (bits 16..31) and, in entry 0, the count (< 2^16 rows per workgroup)
+            const uint32_t tag = (uint32_t)((b + 1) & 0xffff) << 16;
+            const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, tag | (src == 0 ? (uint32_t)s_cnt[pl] : 0u)};
             st_coh16(coh_rsrc(part), (uint32_t)((((size_t)pl * G + g) * KC + src) * sizeof(Cand)), v);
         }
-        drain_stores();
-        sync();  // every wave's stores are drained
+        // The records need no drain (the mergers read them again until their tags are this batch's); what does is
+        // wave 0's export apply, the node rows the mergers read for the candidates' state: every vector memory
+        // operation of wave 0 but its newest -- the record store -- complete
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        sync();  // every wave's record stores issued
         if (wave == 0) {
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
             if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
@@ -1027,6 +1032,8 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         ma.C_in = G; ma.C_out = 1; ma.chunk_input = 1;
         ma.cursor = &ctl->plan[b % kPlanRing]; ma.P = NP; ma.B = P.B;
         ma.p0_known = 1; ma.p0v = p0;
+        ma.tag = (uint32_t)((b + 1) & 0xffff);
+        ma.err = P.err;
         ma.nodes = P.nodes; ma.node_offset = P.node_offset;
         ma.dbg = P.mdbg;
         ma.out_rec = reinterpret_cast<Rec *>(lb);
@@ -1336,7 +1343,8 @@ hipError_t pipe_one(const PipeLaunch &L0, int launch, PipeInfo *info, hipStream_
     if (L.R < 1 || L.R > kMaxLocalRanks || L.base[0] != 0) return hipErrorInvalidValue;
     for (int r = 0; r < L.R; ++r) {
         const PersistArgs &a = L.P[r];
-        if (a.G > kMT || a.B > 64 || a.M * kMS < a.B || L.base[r + 1] - L.base[r] != kCommitWGs + a.G + a.M)
+        if (a.G > kMT || a.B > 64 || a.M * kMS < a.B || L.base[r + 1] - L.base[r] != kCommitWGs + a.G + a.M ||
+            a.rows_per_wg >= 65536)  // (a record's count field is 16 bits)
             return hipErrorInvalidValue;
     }
     hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-COLS = 37
+COLS = 49
 
 
 def main():
