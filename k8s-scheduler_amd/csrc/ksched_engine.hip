@@ -174,6 +174,8 @@ struct ksched_ctx {
     int prog_G = 0, prog_B = 0, prog_rows = 0;
     uint64_t *d_trace = nullptr;  // KSCHED_PERSIST_TRACE: per-batch wall-clock stamps
     int64_t trace_cap = 0;
+    uint64_t *d_trace_wg = nullptr;  // KSCHED_TRACE_WG: per batch and score workgroup {start, arrival}
+    int64_t trace_wg_elems = 0;
     size_t pws_bytes = 0;
     bool persist_stats = false;  // stats come from the Ctl copy queued behind the run
     int64_t persist_B = 0;
@@ -763,6 +765,19 @@ int enqueue_persistent(ksched_ctx *c) {
         a.trace = c->d_trace;
         a.trace_cap = c->trace_cap;
     }
+    if (const char *wgp = std::getenv("KSCHED_TRACE_WG"); wgp && *wgp) {
+        const int64_t elems = (4 * (c->p / B) + 64) * (int64_t)G;
+        if (c->trace_wg_elems < elems) {
+            if (c->d_trace_wg) hipFree(c->d_trace_wg);
+            c->d_trace_wg = nullptr;
+            c->trace_wg_elems = 0;
+            HIPCHK(c, hipMalloc(&c->d_trace_wg, (size_t)elems * 8));
+            c->trace_wg_elems = elems;
+        }
+        HIPCHK(c, hipMemsetAsync(c->d_trace_wg, 0, (size_t)c->trace_wg_elems * 8, c->stream));
+        a.trace_wg = c->d_trace_wg;
+        a.trace_cap = c->trace_wg_elems / G;
+    }
     if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) {
         HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), c->stream));
@@ -986,7 +1001,7 @@ int ksched_destroy(ksched_ctx *c) {
     }
     for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
-    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_xmin);
+    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_trace_wg); hipFree(c->d_xmin);
     for (int r = 0; r < kMaxXchgRanks; ++r)  // a local group's peers are its own contexts' rings, not IPC maps
         if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[r]);
     c->lg.reset();
@@ -1609,6 +1624,20 @@ static int sync_impl(ksched_ctx *c) {
     if (c->persist_stats && c->d_trace && c->diag.trace) {
         print_persist_trace(c);
         print_wg_busy(c);
+    }
+    // KSCHED_TRACE_WG=<path>: the raw per-workgroup stamps ([batches][G] u64: scan start | arrival << 32)
+    if (c->persist_stats && c->d_trace_wg && c->prog_G > 0) {
+        if (const char *wgp = std::getenv("KSCHED_TRACE_WG"); wgp && *wgp) {
+            std::vector<uint64_t> t((size_t)c->trace_wg_elems);
+            if (hipMemcpy(t.data(), c->d_trace_wg, t.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                if (FILE *f = std::fopen(wgp, "wb")) {
+                    const int64_t hdr[2] = {(int64_t)c->prog_G, c->trace_wg_elems / c->prog_G};
+                    std::fwrite(hdr, 8, 2, f);
+                    std::fwrite(t.data(), 8, t.size(), f);
+                    std::fclose(f);
+                }
+            }
+        }
     }
     if (c->persist_stats) {
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);

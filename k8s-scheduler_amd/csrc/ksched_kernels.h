@@ -414,6 +414,9 @@ struct PersistArgs {
     // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
     uint64_t *trace;
     int64_t trace_cap;
+    // optional (KSCHED_TRACE_WG=<path>): per batch and score workgroup {scan start, arrival} as the low and
+    // high 32 bits of the 100 MHz wall clock, [trace_cap][G]
+    uint64_t *trace_wg;
     int64_t *cdbg;  // KSCHED_COMMIT_STAMPS: commit phase cycle sums (CommitArgs::dbg), else null
     int64_t *mdbg;  // KSCHED_MERGE_STAMPS: merge phase cycle sums (MergeArgs::dbg), else null
     // node-sharded (R > 1, one process per GPU): this rank owns global nodes [node_offset, +n_local);

@@ -67,8 +67,11 @@ struct alignas(16) PipeCtl {
     int32_t c_stop;               // commit workgroup
     int32_t s_ex;                 // score role: rows of this batch scored exactly (screened scan)
     int32_t s_scr;                // score role: this batch uses the screened scan
+    // score role: the next batch's loads and export apply, done by wave kSW - 1 during this batch's fold
+    int32_t n_ok, n_err;          // n_ok: they were (commit(b + 1 - kPipeLag) was already published)
+    int64_t n_p0, n_done;
 };
-constexpr size_t kPipeCtlBytes = 64;
+constexpr size_t kPipeCtlBytes = 128;
 static_assert(sizeof(PipeCtl) <= kPipeCtlBytes, "PipeCtl");
 
 __device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const unsigned long long *p,
@@ -166,6 +169,51 @@ __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int
     nd->af[0] = f0; nd->af[1] = f1; nd->af[2] = f2;
     nd->y[0] = recip_or_zero(a0, f0); nd->y[1] = recip_or_zero(a1, f1); nd->y[2] = recip_or_zero(a2, f2);
     nd->ys[0] = screen_recip(a0); nd->ys[1] = screen_recip(a1); nd->ys[2] = screen_recip(a2);
+}
+
+// Pass 1's lower bounds of one step of kSPU rows into the wave's KC slots.  When kSPU is a multiple of KC,
+// row u of the step goes to slot u % KC, which keeps the MAXIMUM of its rows (one v_max per pair instead of
+// an insertion into a sorted list): the KC slots of a wave, and of the 12 waves, are lower bounds of keys of
+// DISTINCT rows, so the KC-th largest of them is at most the KC-th largest key of the workgroup -- a valid
+// L, at most slightly weaker than the KC-th largest of all the rows' bounds (tools/screen_sim.py: c4 exact
+// rows +4 %).  Otherwise a sorted top-KC insertion.
+#ifndef KSCHED_SCORE_PREFETCH
+#define KSCHED_SCORE_PREFETCH 1
+#endif
+#ifndef KSCHED_SLOT_BOUND
+#define KSCHED_SLOT_BOUND 1
+#endif
+template <int KC, int SPU>
+__device__ __forceinline__ void bound_slots(uint32_t (&t)[KC], const uint32_t (&xs)[SPU]) {
+    if constexpr (KSCHED_SLOT_BOUND && SPU % KC == 0) {
+#pragma unroll
+        for (int u = 0; u < SPU; ++u) t[u % KC] = t[u % KC] > xs[u] ? t[u % KC] : xs[u];
+    } else {
+#pragma unroll
+        for (int u = 0; u < SPU; ++u) {
+            uint32_t xv = xs[u];
+#pragma unroll
+            for (int q = 0; q < KC; ++q) {
+                const uint32_t hi = t[q] > xv ? t[q] : xv;
+                xv = t[q] > xv ? xv : t[q];
+                t[q] = hi;
+            }
+        }
+    }
+}
+
+// descending order of KC values (once per batch, before the cross-wave merge)
+template <int KC>
+__device__ __forceinline__ void sort_desc_u32(uint32_t (&t)[KC]) {
+#pragma unroll
+    for (int i = 1; i < KC; ++i) {
+#pragma unroll
+        for (int j = i; j >= 1; --j) {
+            const uint32_t a = t[j - 1], c = t[j];
+            t[j - 1] = a > c ? a : c;
+            t[j] = a > c ? c : a;
+        }
+    }
 }
 
 // t (sorted descending) <- the KC largest of t and u (both sorted descending): the element-wise max of t
@@ -300,6 +348,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         const int64_t j = g + (int64_t)r * G;
         if (j < n) reinterpret_cast<int4 *>(rows + r)[piece] = reinterpret_cast<const int4 *>(P.nodes + j)[piece];
     }
+    if (tid == 0) pc->n_ok = 0;
     sync();
     if (P.screen_ok) {
         for (int r = tid; r < R; r += kST) {  // the screen's f32 reciprocals, one 16-byte record per row
@@ -314,83 +363,105 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     // each workgroup turns it off for a while when most of its rows need the exact score anyway
     constexpr bool kScreen = PRIO == kPrioResource && F53;
     constexpr int kScreenOffBatches = 16;
+    constexpr bool kPrefetch = kSW > 8 && KSCHED_SCORE_PREFETCH;  // wave kSW - 1 does not fold
     int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
     int64_t ex_rows = 0, scan_rows = 0;  // tid 0: rows scored exactly / rows scanned (progress words 4, 5)
     const int64_t Rvalid = (n - g + G - 1) / G;  // rows of this workgroup that hold a node
     int64_t nact = 0;
     int idle = 0;
     unsigned long long early_c = 0;  // wave 0 lane 0: Ctl::committed as read before the last fold
+    unsigned long long pre_c = 0;    // wave kSW - 1 lane 0: the same, for the prefetch of the next batch
+    // One wave's round of loads for batch bb -- lane 0: its plan, the cursor after commit(bb - kPipeLag), the
+    // error word; every lane: that commit's export (count and entries, lane = entry) -- and the apply of the
+    // exported nodes this workgroup owns to its LDS rows and their HBM rows (the mergers read a candidate's
+    // state there, sc1).  The caller has seen commit(bb - kPipeLag) published (stop: it timed out instead).
+    auto load_apply = [&](int64_t bb, int stop, int64_t *p0v, int64_t *donev, int *errv) {
+        int nxv = 0;
+        u32x4 x0 = {0u, 0u, 0u, 0u}, x1 = {0u, 0u, 0u, 0u};  // entry chunks {idx, pad, cur0} {cur1, cur2}
+        const XBuf *xb =
+            reinterpret_cast<const XBuf *>(P.xring + (size_t)((bb >= kPipeLag ? bb - kPipeLag : 0) % 4) * P.xbuf_bytes);
+        if (lane == 0) {
+            *p0v = (int64_t)ld_coh(&ctl->plan[bb % kPlanRing]);
+            *donev = bb >= kPipeLag ? (int64_t)ld_coh(&ctl->cursor_at[(bb - kPipeLag) % kPlanRing]) : 0;
+            // a failed peer (a wait timed out) ends the call for everyone
+            *errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (bb >= kPipeLag && !stop) {
+            // {count, batch tag} in one granule: an idle commit (plan -1) leaves its ring slot untouched,
+            // so a slot still tagged with an older batch is an empty export (never a torn one)
+            const uint64_t hdr = ld_coh(&xb->count);  // one address: one request for the wave
+            nxv = (uint32_t)(hdr >> 32) == (uint32_t)(bb - kPipeLag) ? (int)(uint32_t)hdr : 0;
+            if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
+                const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);  // uniform base, the lane's entry by offset
+                const uint32_t o = (uint32_t)lane * (uint32_t)sizeof(XRec);
+                x0 = ld_coh16(rs, o); x1 = ld_coh16(rs, o + 16);
+            }
+        }
+        auto apply = [&](const u32x4 &c0, const u32x4 &c1) {
+            const int64_t j = (int64_t)(int32_t)c0.x - P.node_offset;  // local row
+            if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
+            const int64_t a0 = (int64_t)(((uint64_t)c0.w << 32) | c0.z), a1 = (int64_t)(((uint64_t)c1.y << 32) | c1.x),
+                          a2 = (int64_t)(((uint64_t)c1.w << 32) | c1.z);
+            set_row(rows + j / G, a0, a1, a2);
+            if (P.screen_ok) ysq[j / G] = make_float4(screen_recip(a0), screen_recip(a1), screen_recip(a2), 0.0f);
+            st_coh(&P.nodes[j].a[0], (uint64_t)a0);
+            st_coh(&P.nodes[j].a[1], (uint64_t)a1);
+            st_coh(&P.nodes[j].a[2], (uint64_t)a2);
+        };
+        if (lane < nxv) apply(x0, x1);
+        for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
+            const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);
+            const uint32_t o = (uint32_t)e * (uint32_t)sizeof(XRec);
+            apply(ld_coh16(rs, o), ld_coh16(rs, o + 16));
+        }
+    };
     for (int64_t b = 0;; ++b) {
-        // ---- wave 0: wait for commit(b - kPipeLag), then ONE round of loads -- its plan for b, the cursor after it,
-        // its export (count and entries, lane = entry) -- and apply the exported nodes this workgroup owns
-        // to its LDS rows before the barrier (the other waves never touch the export) ----
+        // ---- wave 0: wait for commit(b - kPipeLag), then ONE round of loads and the export apply (load_apply),
+        // before the barrier (the other waves never touch the export) -- unless wave kSW - 1 did both during
+        // the previous batch's fold ----
         if (wave == 0) {
-            int stop = 0;
-            if (lane == 0) {
-                unsigned long long seen = 0;
-                const unsigned long long need = (unsigned long long)(b - kPipeLag + 1);
-                // the count read before the previous batch's fold (early_c) usually suffices: no wait, and no
-                // progress store ahead of this round of loads
-                if (b >= kPipeLag && early_c < need) {
-                    prog_at(P, g, b, kProgWaitCommit, 0);
-                    if (!spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, need, &seen)) {
-                        set_err(P.err, 6);
-                        prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
-                        stop = 2;
+            if (kPrefetch && __builtin_amdgcn_readfirstlane(pc->n_ok)) {  // wave kSW - 1 did it during the last fold
+                if (lane == 0) {
+                    pc->s_p0 = pc->n_p0;
+                    pc->s_done = pc->n_done;
+                    pc->s_stop = pc->n_err != 0 ? 3 : 0;
+                    pc->s_scr = kScreen && P.screen_ok && !P.no_screen && b >= scr_off_until;
+                    pc->s_ex = 0;
+                    pc->n_ok = 0;
+                }
+            } else {
+                int stop = 0;
+                if (lane == 0) {
+                    unsigned long long seen = 0;
+                    const unsigned long long need = (unsigned long long)(b - kPipeLag + 1);
+                    // the count read before the previous batch's fold (early_c) usually suffices: no wait, and no
+                    // progress store ahead of this round of loads
+                    if (b >= kPipeLag && early_c < need) {
+                        prog_at(P, g, b, kProgWaitCommit, 0);
+                        if (!spin_ge(P, g, &ctl->committed_x[g % kCtlReplicas].v, need, &seen)) {
+                            set_err(P.err, 6);
+                            prog_at(P, g, b, kProgWaitCommit | kProgTimedOut, seen);
+                            stop = 2;
+                        }
                     }
+                    if (g == 0) trace_at(P, b, 6);
                 }
-                if (g == 0) trace_at(P, b, 6);
-            }
-            stop = __builtin_amdgcn_readfirstlane(stop);
-            int64_t p0v = 0, donev = 0;
-            int errv = 0, nxv = 0;
-            u32x4 x0 = {0u, 0u, 0u, 0u}, x1 = {0u, 0u, 0u, 0u};  // entry chunks {idx, pad, cur0} {cur1, cur2}
-            const XBuf *xb =
-                reinterpret_cast<const XBuf *>(P.xring + (size_t)((b >= kPipeLag ? b - kPipeLag : 0) % 4) * P.xbuf_bytes);
-            if (lane == 0) {
-                p0v = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
-                donev = b >= kPipeLag ? (int64_t)ld_coh(&ctl->cursor_at[(b - kPipeLag) % kPlanRing]) : 0;
-                // a failed peer (a wait timed out) ends the call for everyone
-                errv = __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (b >= kPipeLag && !stop) {
-                // {count, batch tag} in one granule: an idle commit (plan -1) leaves its ring slot untouched,
-                // so a slot still tagged with an older batch is an empty export (never a torn one)
-                const uint64_t hdr = ld_coh(&xb->count);  // one address: one request for the wave
-                nxv = (uint32_t)(hdr >> 32) == (uint32_t)(b - kPipeLag) ? (int)(uint32_t)hdr : 0;
-                if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
-                    const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);  // uniform base, the lane's entry by offset
-                    const uint32_t o = (uint32_t)lane * (uint32_t)sizeof(XRec);
-                    x0 = ld_coh16(rs, o); x1 = ld_coh16(rs, o + 16);
+                stop = __builtin_amdgcn_readfirstlane(stop);
+                int64_t p0v = 0, donev = 0;
+                int errv = 0;
+                load_apply(b, stop, &p0v, &donev, &errv);
+                if (lane == 0) {
+                    pc->s_p0 = p0v;
+                    pc->s_done = donev;
+                    pc->s_stop = errv != 0 ? 3 : stop;
+                    pc->s_scr = kScreen && P.screen_ok && !P.no_screen && b >= scr_off_until;
+                    pc->s_ex = 0;
                 }
-            }
-            auto apply = [&](const u32x4 &c0, const u32x4 &c1) {
-                const int64_t j = (int64_t)(int32_t)c0.x - P.node_offset;  // local row
-                if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
-                const int64_t a0 = (int64_t)(((uint64_t)c0.w << 32) | c0.z), a1 = (int64_t)(((uint64_t)c1.y << 32) | c1.x),
-                              a2 = (int64_t)(((uint64_t)c1.w << 32) | c1.z);
-                set_row(rows + j / G, a0, a1, a2);
-                if (P.screen_ok) ysq[j / G] = make_float4(screen_recip(a0), screen_recip(a1), screen_recip(a2), 0.0f);
-                // the mergers read a candidate's state from its HBM row (sc1)
-                st_coh(&P.nodes[j].a[0], (uint64_t)a0);
-                st_coh(&P.nodes[j].a[1], (uint64_t)a1);
-                st_coh(&P.nodes[j].a[2], (uint64_t)a2);
-            };
-            if (lane < nxv) apply(x0, x1);
-            for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
-                const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);
-                const uint32_t o = (uint32_t)e * (uint32_t)sizeof(XRec);
-                apply(ld_coh16(rs, o), ld_coh16(rs, o + 16));
-            }
-            if (lane == 0) {
-                pc->s_p0 = p0v;
-                pc->s_done = donev;
-                pc->s_stop = errv != 0 ? 3 : stop;
-                pc->s_scr = kScreen && P.screen_ok && !P.no_screen && b >= scr_off_until;
-                pc->s_ex = 0;
             }
         }
         sync();
+        // the prefetch's node-row stores are complete before this batch's arrival (the mergers read them)
+        if (kPrefetch && wave == kSW - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (pc->s_stop) return;
         const int64_t p0 = pc->s_p0;
         if (pc->s_done >= NP) break;  // every pod resolved by commit(b - kPipeLag) or earlier
@@ -410,7 +481,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             if (g == 0) trace_at(P, b, 0);
             prog_at(P, g, b, kProgScan, 0);
         }
-        const uint64_t t_go = (P.trace && tid == 0) ? wall_clock64() : 0;
+        const uint64_t t_go = ((P.trace || P.trace_wg) && tid == 0) ? wall_clock64() : 0;
         // ---- score: lane = pod, wave w scans rows r = w, w + W, ... (nodes j = g + r G) ----
         if (tid < 64) s_cnt[tid] = 0;
         const int64_t pod = p0 + lane;
@@ -512,16 +583,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                             na += anya ? 1 : 0;
                         }
                     }
-#pragma unroll
-                    for (int u = 0; u < kSPU; ++u) {
-                        uint32_t xv = xs[u];
-#pragma unroll
-                        for (int q = 0; q < KC; ++q) {
-                            const uint32_t hi = t[q] > xv ? t[q] : xv;
-                            xv = t[q] > xv ? xv : t[q];
-                            t[q] = hi;
-                        }
-                    }
+                    bound_slots<KC>(t, xs);
                 }
                 // the ambiguous pairs' predicate, exactly
                 for (int e = 0; e < na; ++e) {
@@ -551,21 +613,13 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         cnt += (valid && f) ? 1 : 0;
                         xs[u] = (valid && active && el && lo_ok) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
                     }
-#pragma unroll
-                    for (int u = 0; u < kSPU; ++u) {
-                        uint32_t xv = xs[u];
-#pragma unroll
-                        for (int q = 0; q < KC; ++q) {
-                            const uint32_t hi = t[q] > xv ? t[q] : xv;
-                            xv = t[q] > xv ? xv : t[q];
-                            t[q] = hi;
-                        }
-                    }
+                    bound_slots<KC>(t, xs);
                 }
             }
             if (g == 0 && tid == 0) trace_at(P, b, 11);
             // ---- the workgroup's bound: the KC-th largest lower bound over every wave's list (the fold
             // area is free until the scan ends) ----
+            sort_desc_u32<KC>(t);
 #pragma unroll
             for (int q = 0; q < KC; ++q) sl[(wave * KC + q) * 64 + lane] = t[q];
             sync();
@@ -688,6 +742,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         // the commit count for the next batch's wait, read now: its latency hides behind the fold and stores
         if (tid == 0) early_c = __hip_atomic_load(&ctl->committed_x[g % kCtlReplicas].v, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (kPrefetch && wave == kSW - 1 && lane == 0)
+            pre_c = __hip_atomic_load(&ctl->committed_x[g % kCtlReplicas].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sync();  // every wave's scan is done (the fold area is free); s_cnt was zeroed
         if (g == 0 && tid == 0) trace_at(P, b, 9);
         if (cnt) atomicAdd(&s_cnt[lane], cnt);
@@ -706,6 +762,27 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch (waves 0..7)
         const int src = lane & 7;               // ... and source wave (plus src + 8 when that exists)
         const bool folds = wave < 8;
+        if (kPrefetch && wave == kSW - 1) {
+            // ---- the next batch's loads and export apply, while waves 0..7 fold: a workgroup still busy
+            // with this batch when commit(b + 1 - kPipeLag) is published starts the next scan right after
+            // its arrival.  Only when that commit is already out: this wave never waits for it ----
+            const unsigned long long need = (unsigned long long)(b + 1 - kPipeLag + 1);
+            int ok = 0;
+            if (lane == 0) {
+                ok = b + 1 < kPipeLag || pre_c >= need;
+                if (!ok) ok = __hip_atomic_load(&ctl->committed_x[g % kCtlReplicas].v, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) >= need;
+            }
+            ok = __builtin_amdgcn_readfirstlane(ok);
+            if (ok) {
+                if (g == 0 && lane == 0) trace_at(P, b + 1, 6);
+                int64_t p0v = 0, donev = 0;
+                int errv = 0;
+                load_apply(b + 1, 0, &p0v, &donev, &errv);
+                if (lane == 0) { pc->n_p0 = p0v; pc->n_done = donev; pc->n_err = errv; }
+            }
+            if (lane == 0) pc->n_ok = ok;
+        }
         if (folds) {
 #pragma unroll
             for (int q = 0; q < KC; ++q) {
@@ -763,6 +840,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 if (old + 1 == (use + 1) * (unsigned long long)G) trace_at(P, b, 1);
                 prog_at(P, g, b, kProgArrived, old + 1);
                 if (P.trace) prog_add(P, g, t_scan - t_go, wall_clock64() - t_go);
+                if (P.trace_wg && b < P.trace_cap)
+                    P.trace_wg[b * G + g] = (t_go & 0xffffffffull) | (wall_clock64() << 32);
             }
         }
         // the next batch's first barrier orders s_cnt / fold reuse after wave 0's reads
