@@ -288,6 +288,19 @@ __device__ __forceinline__ float screen_q(float c, float m, float p, bool okc, b
     return v;
 }
 
+// The screened scan's per-pair record (pass 1 -> pass 2): an upper bound of a screen value v (<= 10; NaN
+// allowed) in 16 bits, q = floor(4096 RN(10 - v)) clamped at 0 (NaN and negatives -> 0; the
+// fma is RN(40960 - 4096 v) = 4096 RN(10 - v) exactly, 4096 v being exact), decoded as
+// RN(10 + 2^-12 - q 2^-12) >= v: RN(10 - v) exceeds 10 - v by at most 2^-21 (tests/test_screen_bound.py).
+// q = 0 decodes to the largest bound (10 + 2^-12, always needed), 0xffff to ~ -6 (never needed).
+__device__ __forceinline__ uint32_t screen_rec(float v) {
+    const float x = __builtin_fmaxf(__builtin_fmaf(-4096.0f, v, 40960.0f), 0.0f);  // NaN -> 0 (maxNum)
+    return (uint32_t)x;
+}
+__device__ __forceinline__ float screen_rec_bound(uint32_t q) {
+    return __builtin_fmaf((float)q, -0x1p-12f, 10.0f + 0x1p-12f);
+}
+
 // The screen of one pair.  ok* = (a_k >= r_k) per resource (exact int64 compares).  Returns the f32 value
 // (NaN: unscreenable, every comparison then asks for the exact score); *lo_ok: the pair surely carries an
 // eligible key >= value - eps (its value may serve as a lower bound: a polynomial pair with a fraction near 1

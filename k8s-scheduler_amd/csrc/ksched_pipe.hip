@@ -291,7 +291,7 @@ struct ScoreLayout {
     // the screened scan (when it fits): its f32 reciprocals, one 16-byte record per row ...
     __host__ __device__ static size_t ysq_off(int R) { return total(R); }
     __host__ __device__ static size_t total_screen(int R) { return total(R) + (size_t)R * 16; }
-    // ... and pass 1's per-pair records for pass 2: [kSW][ceil(R / kSW)][64] f16
+    // ... and pass 1's per-pair records for pass 2: [kSW][ceil(R / kSW)][64] u16 (screen_rec)
     __host__ __device__ static size_t hrec_off(int R) { return total_screen(R); }
     // rows per wave, rounded up to pairs (pass 1 stores the records of two rows in one 32-bit word)
     __host__ __device__ static int hrec_qw(int R) { return ((R + kSW - 1) / kSW + 1) / 2 * 2; }
@@ -524,7 +524,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 return screen_q(c, m, p, okc, okm, okp, lo_ok);
             };
             // ---- pass 1: every row -- the predicate count, the KC largest lower bounds of this pod's eligible
-            // keys, and (keep_h) the pair's upper bound as an f16 record for pass 2 ----
+            // keys, and (keep_h) the pair's upper bound as a 16-bit record for pass 2 ----
             uint32_t t[KC];
 #pragma unroll
             for (int q = 0; q < KC; ++q) t[q] = 0u;
@@ -563,11 +563,9 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const float v = screen_q(c, m, p, okc, okm, okp, &lo_ok);
                         cnt += (valid && f && !amb) ? 1 : 0;
                         xs[u] = (valid && active && el && lo_ok && !amb) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
-                        // 10 - h >= v: h = f16 of (10 - v), rounded down by a relative 2^-10 and 2^-24 absolute
-                        // (f16 rounding is within 2^-11 relative); +inf (never needed) without a key; NaN stays NaN
-                        const float w = 10.0f - v;
-                        const float wd = w - __builtin_fabsf(w) * 0x1p-10f - 0x1p-24f;
-                        hh[u] = __half_as_ushort(__float2half_rn(amb ? __builtin_nanf("") : (el ? wd : __builtin_inff())));
+                        // the pair's upper bound (screen_rec): 0 (always needed) when ambiguous, 0xffff (never
+                        // needed) without a key
+                        hh[u] = amb ? 0u : (el ? screen_rec(v) : 0xffffu);
                         ambm |= (valid && amb) ? 1u << u : 0u;
                     }
                     // the records of rows k, k + 1 (k = (r0 - wave) / kSW + u, u even) in one store; a pair's second
@@ -648,7 +646,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                     }
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const float vd = 10.0f - __half2float(__ushort_as_half(hv[u]));
+                        const float vd = screen_rec_bound(hv[u]);
                         const bool need = i0 + u < nr && active && !(vd + (1.0f + kScreenEps) < L);  // NaN: needed
                         const bool any = __ballot(need) != 0;
                         // kept when any; an index past QW only on a row past the wave's last (never kept)

@@ -158,3 +158,39 @@ def test_unscreenable_values_are_nan():
     s, _ = screen_score([-5, 1, 1, 1], [1, 1 << 53, 1, 1], [1, 1, 1, 1], [10, 10, 0, -3], [10, 1 << 60, 10, 10],
                         [10, 10, 10, 10])
     assert np.all(np.isnan(s))
+
+
+def screen_rec(v):
+    """ksched_device.h screen_rec: q = floor(RN(40960 - 4096 v)) clamped at 0 (NaN -> 0), emulated exactly:
+    40960 - 4096 v is exact in f64, its f32 rounding is the device fma's single rounding."""
+    v = np.asarray(v, np.float32)
+    with np.errstate(invalid="ignore"):
+        x = (np.float64(40960.0) - np.float64(4096.0) * v.astype(np.float64)).astype(np.float32)
+        q = np.where(np.isnan(x) | (x < 0), 0, np.floor(x)).astype(np.int64)
+    return q
+
+
+def screen_rec_bound(q):
+    """ksched_device.h screen_rec_bound: RN(10 + 2^-12 - q 2^-12) (exact in f64, one rounding to f32)."""
+    q = np.asarray(q, np.int64)
+    return (np.float64(10.0) + 2.0 ** -12 - q.astype(np.float64) * 2.0 ** -12).astype(np.float32)
+
+
+def test_screen_record_is_an_upper_bound():
+    rng = np.random.default_rng(7)
+    v = rng.uniform(0, 10, 2_000_000).astype(np.float32)
+    grid = (np.arange(0, 40961, dtype=np.float64) / 4096).astype(np.float32)  # multiples of 2^-12 and neighbours
+    v = np.concatenate([v, grid, np.nextafter(grid, F(0)), np.nextafter(grid, F(11)), F([0.0, 10.0, 1e-30, 9.9999995])])
+    v = v[(v >= 0) & (v <= 10)]
+    # the device's fma equals 4096 * RN(10 - v) bit for bit
+    assert np.array_equal(((F(10.0) - v) * F(4096.0)),
+                          (np.float64(40960.0) - np.float64(4096.0) * v.astype(np.float64)).astype(np.float32))
+    q = screen_rec(v)
+    assert q.min() >= 0 and q.max() <= 40960  # 16 bits, 0xffff stays free for "no key"
+    ub = screen_rec_bound(q)
+    assert np.all(ub >= v)
+    assert np.max(ub.astype(np.float64) - v) <= 2.0 ** -11 + 1e-6  # tight: 2^-12 of slack plus the quantum
+    # NaN (an unscreenable pair) decodes to the largest bound
+    assert screen_rec(F([np.nan]))[0] == 0 and screen_rec_bound(0) >= F(10.0)
+    # "no key" (0xffff) is below every bound L >= 0 even with the pass-2 margin
+    assert screen_rec_bound(0xFFFF) + F(1.0) + EPS < 0
