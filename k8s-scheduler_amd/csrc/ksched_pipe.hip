@@ -636,6 +636,11 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             int qn = 0;
             if (keep_h) {
                 const int nr = (Rv - wave + kSW - 1) / kSW;  // this wave's rows
+                // in the records' own units: the pair is needed when its bound + 1 + eps reaches L, i.e.
+                // 10 + 2^-12 - q 2^-12 + 1 + eps >= L  <=>  q <= 4096 (11 + 2^-12 + eps - L) (exact in f64; one
+                // quantum more keeps the integer test a superset of the real one); -1: an inactive lane
+                const int tq = active ? (int)__builtin_floor(4096.0 * (11.0 + 0x1p-12 + (double)kScreenEps - (double)L)) + 1
+                                      : -1;
                 for (int i0 = 0; i0 < nr; i0 += 8) {
                     uint16_t hv[8];
 #pragma unroll
@@ -644,15 +649,18 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         hv[u] = (uint16_t)x;
                         hv[u + 1] = (uint16_t)(x >> 16);
                     }
+                    uint32_t grp = 0;  // wave-uniform: the group's rows some pod needs
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const float vd = screen_rec_bound(hv[u]);
-                        const bool need = i0 + u < nr && active && !(vd + (1.0f + kScreenEps) < L);  // NaN: needed
-                        const bool any = __ballot(need) != 0;
-                        // kept when any; an index past QW only on a row past the wave's last (never kept)
-                        if (lane == 0 && qn < QW) qrow[wave * QW + qn] = (uint16_t)(wave + (i0 + u) * kSW);
-                        qn += any ? 1 : 0;
+                        const uint64_t bm = __builtin_amdgcn_ballot_w64((int)hv[u] <= tq);
+                        grp |= (bm != 0 ? 1u : 0u) << u;
                     }
+                    if (nr - i0 < 8) grp &= (1u << (nr - i0)) - 1u;  // rows past the wave's last
+                    // lanes 0..7 queue the group's needed rows in order, one store (a wave's rows fit its QW)
+                    if (lane < 8 && ((grp >> lane) & 1u))
+                        qrow[wave * QW + qn + __builtin_popcount(grp & ((1u << lane) - 1u))] =
+                            (uint16_t)(wave + (i0 + lane) * kSW);
+                    qn += __builtin_popcount(grp);
                 }
             } else {
                 for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {

@@ -194,3 +194,22 @@ def test_screen_record_is_an_upper_bound():
     assert screen_rec(F([np.nan]))[0] == 0 and screen_rec_bound(0) >= F(10.0)
     # "no key" (0xffff) is below every bound L >= 0 even with the pass-2 margin
     assert screen_rec_bound(0xFFFF) + F(1.0) + EPS < 0
+
+
+def test_pass2_integer_threshold_is_a_superset():
+    """Pass 2 tests q <= tq, tq = floor(4096 (11 + 2^-12 + eps - L)) + 1 (f64), instead of decoding every
+    record: every pair whose decoded bound + 1 + eps reaches L (exactly, and in the f32 form the kernel used
+    before) must pass, and the test may admit at most two quanta more."""
+    rng = np.random.default_rng(11)
+    L = np.concatenate([rng.uniform(0, 11, 20000), F([0.0, 1.0, 11.0])]).astype(np.float32)
+    q = rng.integers(0, 40961, L.size)
+    tq = np.floor(4096.0 * (11.0 + 2.0 ** -12 + np.float64(EPS) - L.astype(np.float64))).astype(np.int64) + 1
+    ub = screen_rec_bound(q)
+    real_need = (10.0 + 2.0 ** -12 - q * 2.0 ** -12) + 1.0 + np.float64(EPS) >= L.astype(np.float64)
+    f32_need = ~((ub + (F(1.0) + EPS)) < L)
+    got = q <= tq
+    assert np.all(got[real_need]) and np.all(got[f32_need])
+    assert np.all(q[got] <= tq[got]) and not np.any(got & (q < tq - 2) & ~real_need)
+    # L = 0 (fewer than KC bounds): every pair with a key passes, none without one (0xffff)
+    t0 = int(np.floor(4096.0 * (11.0 + 2.0 ** -12 + np.float64(EPS)))) + 1
+    assert 40960 <= t0 < 0xFFFF
