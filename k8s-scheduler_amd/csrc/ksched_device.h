@@ -288,17 +288,25 @@ __device__ __forceinline__ float screen_q(float c, float m, float p, bool okc, b
     return v;
 }
 
-// The screened scan's per-pair record (pass 1 -> pass 2): an upper bound of a screen value v (<= 10; NaN
-// allowed) in 16 bits, q = floor(4096 RN(10 - v)) clamped at 0 (NaN and negatives -> 0; the
-// fma is RN(40960 - 4096 v) = 4096 RN(10 - v) exactly, 4096 v being exact), decoded as
-// RN(10 + 2^-12 - q 2^-12) >= v: RN(10 - v) exceeds 10 - v by at most 2^-21 (tests/test_screen_bound.py).
-// q = 0 decodes to the largest bound (10 + 2^-12, always needed), 0xffff to ~ -6 (never needed).
+// The screened scan's per-pair record (pass 1 -> pass 2): a 16-bit upper bound of a screen value v (<= 10; NaN
+// allowed), 10 - value(h) >= v - 2^-21, as the f16 bit pattern h of w = RN(10 - v) rounded DOWN (RN, then one
+// ulp less when that rounded up; NaN -> w = 0, always needed).  w >= 0, so patterns order as values and pass 2
+// compares them as integers against screen_rec_threshold; f16's relative precision keeps the bound tight where
+// the keys crowd (v near 10, small w).  0xffff: no key (above every threshold).
 __device__ __forceinline__ uint32_t screen_rec(float v) {
-    const float x = __builtin_fmaxf(__builtin_fmaf(-4096.0f, v, 40960.0f), 0.0f);  // NaN -> 0 (maxNum)
-    return (uint32_t)x;
+    const float w = __builtin_fmaxf(10.0f - v, 0.0f);  // NaN -> 0 (maxNum)
+    const _Float16 h = (_Float16)w;
+    const uint32_t hb = (uint32_t)__builtin_bit_cast(uint16_t, h);
+    return hb - ((float)h > w ? 1u : 0u);
 }
-__device__ __forceinline__ float screen_rec_bound(uint32_t q) {
-    return __builtin_fmaf((float)q, -0x1p-12f, 10.0f + 0x1p-12f);
+// The largest record (+ one) a pod needs with bound L (shifted by +1, 0 = none): 10 - value(h) + 2^-20 + 1 + eps
+// >= L  <=>  value(h) <= T = 11 + eps + 2^-20 - L; -1 when T < 0.  RN to f16 of T (as f32), plus one pattern:
+// a superset of the exact test (tests/test_screen_bound.py)
+__device__ __forceinline__ int screen_rec_threshold(float L) {
+    const double T = 11.0 + (double)kScreenEps + 0x1p-20 - (double)L;
+    if (!(T >= 0.0)) return -1;
+    const _Float16 h = (_Float16)(float)T;
+    return (int)__builtin_bit_cast(uint16_t, h) + 1;
 }
 
 // The screen of one pair.  ok* = (a_k >= r_k) per resource (exact int64 compares).  Returns the f32 value

@@ -636,11 +636,9 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             int qn = 0;
             if (keep_h) {
                 const int nr = (Rv - wave + kSW - 1) / kSW;  // this wave's rows
-                // in the records' own units: the pair is needed when its bound + 1 + eps reaches L, i.e.
-                // 10 + 2^-12 - q 2^-12 + 1 + eps >= L  <=>  q <= 4096 (11 + 2^-12 + eps - L) (exact in f64; one
-                // quantum more keeps the integer test a superset of the real one); -1: an inactive lane
-                const int tq = active ? (int)__builtin_floor(4096.0 * (11.0 + 0x1p-12 + (double)kScreenEps - (double)L)) + 1
-                                      : -1;
+                // in the records' own units: the pair is needed when its bound + 1 + eps reaches L; -1: an
+                // inactive lane
+                const int tq = active ? screen_rec_threshold(L) : -1;
                 for (int i0 = 0; i0 < nr; i0 += 8) {
                     uint16_t hv[8];
 #pragma unroll

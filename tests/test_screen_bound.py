@@ -160,56 +160,58 @@ def test_unscreenable_values_are_nan():
     assert np.all(np.isnan(s))
 
 
+
 def screen_rec(v):
-    """ksched_device.h screen_rec: q = floor(RN(40960 - 4096 v)) clamped at 0 (NaN -> 0), emulated exactly:
-    40960 - 4096 v is exact in f64, its f32 rounding is the device fma's single rounding."""
+    """ksched_device.h screen_rec: the f16 pattern of w = max(RN(10 - v), 0) rounded down (NaN -> 0)."""
     v = np.asarray(v, np.float32)
     with np.errstate(invalid="ignore"):
-        x = (np.float64(40960.0) - np.float64(4096.0) * v.astype(np.float64)).astype(np.float32)
-        q = np.where(np.isnan(x) | (x < 0), 0, np.floor(x)).astype(np.int64)
-    return q
+        w = np.fmax(F(10.0) - v, F(0.0))
+    h = w.astype(np.float16)  # round to nearest even, like v_cvt_f16_f32
+    hb = h.view(np.uint16).astype(np.int64)
+    return hb - (h.astype(np.float32) > w)
 
 
-def screen_rec_bound(q):
-    """ksched_device.h screen_rec_bound: RN(10 + 2^-12 - q 2^-12) (exact in f64, one rounding to f32)."""
-    q = np.asarray(q, np.int64)
-    return (np.float64(10.0) + 2.0 ** -12 - q.astype(np.float64) * 2.0 ** -12).astype(np.float32)
+def rec_value(hb):
+    return np.asarray(hb, np.int64).astype(np.uint16).view(np.float16).astype(np.float64)
+
+
+def screen_rec_threshold(L):
+    """ksched_device.h screen_rec_threshold."""
+    L = np.asarray(L, np.float32)
+    T = 11.0 + np.float64(EPS) + 2.0 ** -20 - L.astype(np.float64)
+    h = T.astype(np.float32).astype(np.float16)
+    return np.where(T >= 0, h.view(np.uint16).astype(np.int64) + 1, -1)
 
 
 def test_screen_record_is_an_upper_bound():
     rng = np.random.default_rng(7)
-    v = rng.uniform(0, 10, 2_000_000).astype(np.float32)
-    grid = (np.arange(0, 40961, dtype=np.float64) / 4096).astype(np.float32)  # multiples of 2^-12 and neighbours
+    v = np.concatenate([rng.uniform(0, 10, 2_000_000), 10 - rng.uniform(0, 0.5, 500_000) ** 2]).astype(np.float32)
+    h16 = np.arange(0, 0x4900 + 1, dtype=np.uint16).view(np.float16).astype(np.float32)  # every f16 in [0, 10]
+    grid = np.float32(10.0) - h16
     v = np.concatenate([v, grid, np.nextafter(grid, F(0)), np.nextafter(grid, F(11)), F([0.0, 10.0, 1e-30, 9.9999995])])
     v = v[(v >= 0) & (v <= 10)]
-    # the device's fma equals 4096 * RN(10 - v) bit for bit
-    assert np.array_equal(((F(10.0) - v) * F(4096.0)),
-                          (np.float64(40960.0) - np.float64(4096.0) * v.astype(np.float64)).astype(np.float32))
-    q = screen_rec(v)
-    assert q.min() >= 0 and q.max() <= 40960  # 16 bits, 0xffff stays free for "no key"
-    ub = screen_rec_bound(q)
-    assert np.all(ub >= v)
-    assert np.max(ub.astype(np.float64) - v) <= 2.0 ** -11 + 1e-6  # tight: 2^-12 of slack plus the quantum
-    # NaN (an unscreenable pair) decodes to the largest bound
-    assert screen_rec(F([np.nan]))[0] == 0 and screen_rec_bound(0) >= F(10.0)
-    # "no key" (0xffff) is below every bound L >= 0 even with the pass-2 margin
-    assert screen_rec_bound(0xFFFF) + F(1.0) + EPS < 0
+    hb = screen_rec(v)
+    assert hb.min() >= 0 and hb.max() <= 0x4900  # 16 bits, 0xffff stays free for "no key"
+    ub = 10.0 - rec_value(hb)  # the bound pass 2 implies, before its 2^-20 slack
+    assert np.all(ub + 2.0 ** -21 >= v)
+    w = 10.0 - v.astype(np.float64)
+    assert np.all(10.0 - ub <= w + 2.0 ** -21) and np.all(10.0 - ub >= w * (1 - 2.0 ** -10) - 2.0 ** -24 - 2.0 ** -21)
+    assert screen_rec(F([np.nan]))[0] == 0  # an unscreenable pair: always needed
 
 
 def test_pass2_integer_threshold_is_a_superset():
-    """Pass 2 tests q <= tq, tq = floor(4096 (11 + 2^-12 + eps - L)) + 1 (f64), instead of decoding every
-    record: every pair whose decoded bound + 1 + eps reaches L (exactly, and in the f32 form the kernel used
-    before) must pass, and the test may admit at most two quanta more."""
+    """Pass 2 tests hb <= screen_rec_threshold(L) instead of decoding every record: every pair whose bound
+    10 - value(hb) (+ the 2^-21 of w's own rounding) + 1 + eps reaches L must pass."""
     rng = np.random.default_rng(11)
-    L = np.concatenate([rng.uniform(0, 11, 20000), F([0.0, 1.0, 11.0])]).astype(np.float32)
-    q = rng.integers(0, 40961, L.size)
-    tq = np.floor(4096.0 * (11.0 + 2.0 ** -12 + np.float64(EPS) - L.astype(np.float64))).astype(np.int64) + 1
-    ub = screen_rec_bound(q)
-    real_need = (10.0 + 2.0 ** -12 - q * 2.0 ** -12) + 1.0 + np.float64(EPS) >= L.astype(np.float64)
-    f32_need = ~((ub + (F(1.0) + EPS)) < L)
-    got = q <= tq
-    assert np.all(got[real_need]) and np.all(got[f32_need])
-    assert np.all(q[got] <= tq[got]) and not np.any(got & (q < tq - 2) & ~real_need)
+    L = np.concatenate([rng.uniform(0, 11.001, 40000), 11 - rng.uniform(0, 0.3, 20000) ** 2, F([0.0, 1.0, 11.0])]).astype(np.float32)
+    hb = np.concatenate([rng.integers(0, 0x4901, 40000), rng.integers(0, 0x3000, 20003)])
+    tq = screen_rec_threshold(L)
+    need = (10.0 - rec_value(hb)) + 2.0 ** -21 + 1.0 + np.float64(EPS) >= L.astype(np.float64)
+    got = hb <= tq
+    assert np.all(got[need])
+    # tight: admitted beyond the exact test only within two f16 steps of the threshold
+    extra = got & ~need
+    assert np.all(rec_value(hb[extra]) <= (11.0 + np.float64(EPS) + 2.0 ** -20 - L[extra]) * (1 + 2.0 ** -9) + 2.0 ** -23)
     # L = 0 (fewer than KC bounds): every pair with a key passes, none without one (0xffff)
-    t0 = int(np.floor(4096.0 * (11.0 + 2.0 ** -12 + np.float64(EPS)))) + 1
-    assert 40960 <= t0 < 0xFFFF
+    t0 = int(screen_rec_threshold(F([0.0]))[0])
+    assert 0x4900 <= t0 < 0xFFFF
