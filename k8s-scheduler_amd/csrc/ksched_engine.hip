@@ -200,8 +200,9 @@ struct ksched_ctx {
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
-        int rescue_max = 2;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
+        int rescue_max = 4;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
                                  // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
+                                 // (the budget table)
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
     } diag;
 };
@@ -943,7 +944,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
     c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
-    c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 2);
+    c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane
