@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 5
+#define KSCHED_ABI_VERSION 6
 
 /* status codes */
 #define KSCHED_OK 0
@@ -82,8 +82,9 @@ typedef struct ksched_opts {
     int32_t commit_impl;  /* batched mode: KSCHED_COMMIT_* (0 = auto: speculative when batch <= 64) */
     int32_t pipeline;     /* batched mode: KSCHED_PIPELINE_AUTO (0) or KSCHED_PIPELINE_STREAM (ABI 4) */
     int32_t pipe_wgs;     /* persistent pipeline: at most this many workgroups, one per CU (0 = every CU).
-                             Ranks that share ONE device (a test rehearsal of the multi-GPU path) split its
-                             CUs with it; the launch is then a plain one instead of a cooperative one. (ABI 4) */
+                             The launch is always cooperative (the runtime admits the grid only if every
+                             workgroup is resident at once); ranks that share ONE device are joined by
+                             ksched_xchg_join_local and split its CUs in one such launch. (ABI 4) */
     int32_t reserved[1];
 } ksched_opts;
 
@@ -139,13 +140,18 @@ int ksched_set_comm(ksched_ctx *ctx, const uint8_t id[128]);
  * pipeline's merger workgroups write each pod's candidate list straight into every rank's receive
  * ring over xGMI (tagged 8-byte granules in uncached device memory) and rank-merge the R lists they
  * receive -- no launch, no host round trip, no collective per batch.  Setup, on every rank:
- *   ksched_xchg_export(ctx, h)          allocates this rank's ring; h = its IPC handle
- *   (all-gather the R handles in rank order, e.g. torch.distributed)
- *   ksched_xchg_import(ctx, handles)    maps every rank's ring (R * 64 bytes, own entry ignored)
+ *   ksched_xchg_export(ctx, h)          allocates (or reuses) this rank's ring and zeroes it (a device kernel
+ *                                       of system-scope stores, the granules' own path) at EVERY export;
+ *                                       h = its IPC handle and the first granule tag this process has never
+ *                                       used (128 bytes)
+ *   (all-gather the R blobs in rank order, e.g. torch.distributed)
+ *   ksched_xchg_import(ctx, handles)    maps every rank's ring (R * 128 bytes, own entry ignored); the tags
+ *                                       of the setup start at the largest of the R hints, so no tag repeats
+ *                                       in any process's memory
  * Batched runs then take the exchange path on every rank (an RCCL communicator is optional: it is
  * the fallback when a device timeout disables the exchange; ksched_xchg_ready reports the state).
  * Replaces the same all-gather as ksched_set_comm; the call sequence is unchanged. */
-#define KSCHED_XCHG_HANDLE_BYTES 64
+#define KSCHED_XCHG_HANDLE_BYTES 128
 int ksched_xchg_export(ksched_ctx *ctx, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]);
 int ksched_xchg_import(ksched_ctx *ctx, const uint8_t *handles);
 int ksched_xchg_ready(const ksched_ctx *ctx);
@@ -153,12 +159,22 @@ int ksched_xchg_ready(const ksched_ctx *ctx);
  * any rank failed to import (ABI 4): the ranks must agree on the transport. */
 int ksched_xchg_close(ksched_ctx *ctx);
 /* Ranks as threads of ONE process on ONE device (ABI 5): joins ctxs[0..n-1] (rank r at ctxs[r], each created
- * with nranks = n, 2 <= n <= 4, batch <= 64 and the same options) into the device exchange without IPC.  Their
- * persistent pipelines then run as ONE cooperative launch -- rank r's workgroups a contiguous block range, the
- * ranks sharing the CUs equally -- so every rank's grid is resident at once by construction; separate launches
- * (of separate processes) sharing a device guarantee no such thing.  The contexts' threads
- * call ksched_run concurrently, as with ksched_set_group; destroy all of them together. */
+ * with nranks = n, 2 <= n <= 8, batch <= 64 and the same options) into the device exchange.  Their persistent
+ * pipelines then run as ONE cooperative launch -- rank r's workgroups a contiguous block range, the ranks sharing
+ * the CUs equally -- so every rank's grid is resident at once by construction; separate launches (of separate
+ * processes) sharing a device guarantee no such thing.  The contexts' threads call
+ * ksched_run concurrently, as with ksched_set_group; destroy all of them together.  Every rank's grid must fit
+ * its share of the CUs: at 8 ranks on one MI355X (31 CUs each) that needs batch <= 32.
+ * ksched_xchg_join_local_ex (ABI 6) takes flags: KSCHED_XCHG_RINGS_UNCACHED allocates the rings exactly as
+ * ksched_xchg_export does (hipDeviceMallocUncached, zeroed at every setup, tags from the process's next unused
+ * one); KSCHED_XCHG_RINGS_IPC
+ * (implies UNCACHED) also maps every peer's ring through its IPC handle, as ksched_xchg_import does -- the
+ * multi-process transport's allocation, zeroing, handles and epoch rule on one device (it fails where the
+ * runtime does not open a handle of the same process). */
 int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n);
+#define KSCHED_XCHG_RINGS_UNCACHED 1
+#define KSCHED_XCHG_RINGS_IPC 2
+int ksched_xchg_join_local_ex(ksched_ctx *const *ctxs, int32_t n, int32_t flags);
 
 typedef struct ksched_group ksched_group;
 int ksched_group_create(int32_t nranks, int32_t device, ksched_group **out);

@@ -35,6 +35,8 @@ constexpr int kSpcHash = 1 << kSpcHashBits;
 // two previous batches (lag 3: the persistent pipeline), <= 64 each, + this batch's (<= 64)
 template <bool LAG3>
 constexpr int spc_slots() { return LAG3 ? 192 : 128; }
+// commit_rescue publishes the touched set, at most every slot: RescueReq::ti holds them
+static_assert(spc_slots<true>() + 1 <= kRescueMaxT, "RescueReq::ti must hold the persistent commit's touched slots");
 constexpr int kSpcInvalid = kSpcHash - 1;  // table position reserved for "no entry" (always taken)
 constexpr int kGS = 14;                     // words per guessed entry in SpcSmem::GS
 
@@ -150,6 +152,71 @@ struct RescueOut {
     float price;
 };
 
+// Node-sharded rescue (R > 1; wave 0 of the commit, o = this rank's best): every rank's commit made the same
+// request q (the ranks replay one ordered commit), and each rank's merger slots scanned only its own shard.  The
+// rank's best travels to every rank's ring -- rescue area slot (q % 2, this rank) as 14 tagged 8-byte granules
+// {word, epoch0 + q} (two parities: a rank can be one request ahead of a peer still reading the last one, never
+// two) -- and the R bests fold the same way on every rank (lane = source rank, (key desc, idx asc)).  Restated by
+// oracle/cpu_ref.c or_schedule_lagged_rescue2 (shards).  false: a peer's record never came (error 12).
+__device__ __forceinline__ bool rescue_rank_fold(const PersistArgs &X, unsigned long long q, int64_t timeout_ticks,
+                                                 int32_t *err, RescueOut *o) {
+    const int lane = threadIdx.x & 63;
+    const int R = X.R;
+    const uint32_t tag = X.epoch0 + (uint32_t)q;
+    const size_t off = xchg_rescue_off(R, X.B, (size_t)X.xchg_stride) +
+                       ((size_t)(q & 1) * R) * kXchgRescueRec;
+    Rec mine{};
+    mine.key = o->key; mine.idx = o->idx; mine.valid = o->idx != kNoIdx ? 1 : 0;
+    mine.a[0] = o->a[0]; mine.a[1] = o->a[1]; mine.a[2] = o->a[2];
+    mine.labels = o->labels; mine.price = o->price; mine.pad = 0;
+    const uint32_t *mw = reinterpret_cast<const uint32_t *>(&mine);
+    // lane r < R: this rank's record into rank r's ring (word by word: the words are wave-uniform)
+    if (lane < R) {
+        uint64_t *dst = reinterpret_cast<uint64_t *>(X.rx_peer[lane] + off + (size_t)X.rank * kXchgRescueRec);
+#pragma unroll
+        for (int i = 0; i < kXchgRescueWords; ++i)
+            __hip_atomic_store(dst + i, (uint64_t)mw[i] | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // lane r < R: rank r's record from this rank's own ring
+    uint32_t rw[kXchgRescueWords];
+    bool ok = true;
+    if (lane < R) {
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(X.rx_peer[X.rank] + off + (size_t)lane * kXchgRescueRec);
+        const uint64_t t0 = wall_clock64();
+#pragma unroll
+        for (int i = 0; i < kXchgRescueWords; ++i) {
+            uint64_t v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            while (ok && (uint32_t)(v >> 32) != tag) {
+                if ((int64_t)(wall_clock64() - t0) > timeout_ticks) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+                v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            rw[i] = (uint32_t)v;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < kXchgRescueWords; ++i) rw[i] = 0;
+    }
+    if (__ballot(!ok)) {
+        if (lane == 0) atomicCAS(err, 0, 12);
+        return false;
+    }
+    Rec rr;
+    uint32_t *rp = reinterpret_cast<uint32_t *>(&rr);
+#pragma unroll
+    for (int i = 0; i < kXchgRescueWords; ++i) rp[i] = rw[i];
+    double k = (lane < R && rr.valid) ? rr.key : -__builtin_inf();
+    int32_t ix = (lane < R && rr.valid) ? rr.idx : kNoIdx;
+    int32_t src = lane;
+    wave_argbest(k, ix, src);
+    o->key = k;
+    o->idx = ix;
+    for (int r = 0; r < 3; ++r) o->a[r] = rl64(rr.a[r], src);
+    o->labels = (uint64_t)rl64((int64_t)rr.labels, src);
+    o->price = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(rr.price), src));
+    return true;
+}
+
 // The rescue of pod f's exhausted candidate list (wave 0 of the persistent commit; pod f's list is cut, every
 // entry is touched and no touched node beats its last entry, so the best untouched node may lie outside it):
 // publish the request -- pod f's request and the touched set T = ti[0, nT) -- as sc1 stores, drained, then the
@@ -200,6 +267,7 @@ __device__ __forceinline__ bool commit_rescue(const CommitArgs &A, int f, int64_
     for (int r = 0; r < 3; ++r) o->a[r] = rl64((int64_t)w[2 + r], src);
     o->labels = (uint64_t)rl64((int64_t)w[5], src);
     o->price = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w[6], src));
+    if (A.xp && A.xp->R > 1) return rescue_rank_fold(*A.xp, q, A.timeout_ticks, A.err, o);
     return true;
 }
 
@@ -231,7 +299,8 @@ struct NoWait {
 };
 // The persistent pipeline's hand-off from commit(b - 1) (the other commit workgroup) to commit(b): called by every
 // thread; waits until commit(b - 1) has published, then returns what it left (0), the end of the call (1) or a
-// timeout (-1).  The stream pipeline's single commit kernel needs none.
+// timeout (-1), and to lane e < n1 of wave 0 entry e of export(b - 1).  The stream pipeline's single commit kernel
+// needs none.
 struct HandoffRes {
     int64_t cursor;     // first unresolved pod after commit(b - 1)
     int64_t plan_next;  // the plan of batch b + kPipeLag - 1, set by commit(b - 1)
@@ -240,9 +309,10 @@ struct HandoffRes {
     int32_t pad;
 };
 struct NoHandoff {
-    __device__ int operator()(HandoffRes *) const { return 0; }
+    __device__ int operator()(HandoffRes *, XRec *) const { return 0; }
 };
-// commit(b)'s hand-off record for commit(b + 1) (one lane; every store it describes already drained)
+// commit(b)'s hand-off record for commit(b + 1) (one lane).  Its stores need not be drained first: both granules
+// and every chunk of the export it announces carry the tag, and commit(b + 1) polls them all
 __device__ __forceinline__ void put_handoff(Ctl *ctl, int64_t batch, int n1, int64_t cursor, int64_t rseq, int64_t plan_next) {
     const __amdgpu_buffer_rsrc_t r = coh_rsrc(&ctl->hrec);
     const uint32_t tag = (uint32_t)(batch + 1);
@@ -275,7 +345,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             // reading the slot's previous export: ADVICE r3.)
             if (!wait()) return 0;
             HandoffRes ho;
-            const int hr = handoff(&ho);
+            XRec hx;
+            const int hr = handoff(&ho, &hx);
             if (hr != 0) return hr < 0 ? 0 : 2;
             if (wave == 0) {
                 if (lane == 0) {
@@ -283,7 +354,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;
                     L->rseq = ho.rseq;
                     persist_plan(A, false, ho.cursor);
-                    drain_stores();  // the plan before the record
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
@@ -502,8 +572,9 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             if (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) m.S[(size_t)(i >> 6) * kSpcRow + (i & 63)] = x2v[u];
         }
         // ---- the hand-off: commit(b - 1) published (a workgroup barrier) ----
+        // (wave 0 lane e < n1 receives entry e of export(b - 1) with the record: the same round of loads)
         HandoffRes ho;
-        const int hr = handoff(&ho);
+        const int hr = handoff(&ho, &xi);
         if (hr != 0) return hr < 0 ? 0 : 2;  // timed out / the end of the call (or another workgroup's error)
         if (tid == 0) {
             L->cursor = ho.cursor;
@@ -516,7 +587,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&A.ctl->stats[3]), 1ull,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     persist_plan(A, false, ho.cursor);
-                    drain_stores();  // the plan before the record
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
@@ -524,7 +594,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             return 1;
         }
         n1 = ho.n1;
-        if (wave == 0 && lane < n1) xi = load_xrec<COH>(A.xin->e, lane);
         // P2: export(b - 1).  A node export(b - 2) holds too keeps that slot (its state and key superseded: x2s = -1);
         // the others take slots [n2, nin)
         if (wave == 0) {
@@ -975,7 +1044,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             o.cur[0] = x.cur[0]; o.cur[1] = x.cur[1]; o.cur[2] = x.cur[2];
             o.labels = x.labels; o.price = x.price; o.pad2 = 0;
             const int slot = base + __popcll(mask & ((1ull << lane) - 1));
-            store_xrec<COH>(A.xout->e, slot, o);
+            store_xrec<COH>(A.xout->e, slot, o, (uint32_t)(A.batch + 1));
         }
         base += __popcll(mask);
     }
@@ -984,7 +1053,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
             L->cursor = p0 + done;
             persist_plan(A, done < nb, p0 + done);
-            drain_stores();  // the export and the plan before the record that announces them
+            // no drain in front of the record: commit(b + 1) polls the record and the export's tagged chunks in
+            // one round of loads (the plan reaches the score workgroups behind publish_committed's drain)
             put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
         } else {
             A.xout->count = base;

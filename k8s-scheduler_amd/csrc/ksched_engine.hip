@@ -180,9 +180,11 @@ struct ksched_ctx {
     bool persist_stats = false;  // stats come from the Ctl copy queued behind the run
     int64_t persist_B = 0;
     // device-side candidate exchange of the node-sharded persistent pipeline (ksched_xchg_*)
-    void *d_rx = nullptr;          // this rank's receive ring (uncached device memory)
+    void *d_rx = nullptr;          // this rank's receive ring (rx_prepare)
     size_t rx_bytes = 0;
+    bool rx_uncached = false;      // d_rx is hipDeviceMallocUncached memory (xchg_export's kind)
     char *rx_peer[kMaxXchgRanks] = {};  // every rank's ring as mapped here (own = d_rx)
+    bool rx_ipc[kMaxXchgRanks] = {};    // rx_peer[r] was opened by hipIpcOpenMemHandle (closed by rx_unmap_peers)
     bool xchg_ready = false;       // rings imported: batched runs take the persistent multi-rank path
     bool xchg_run = false;         // the current run uses the exchange
     uint32_t xchg_epoch = 1;       // granule tag base of the next call (identical on every rank)
@@ -334,6 +336,62 @@ void fill_xchg_args(const ksched_ctx *c, PersistArgs *a) {
     a->epoch0 = c->xchg_epoch;
     a->xchg_stride = (int64_t)xchg_stride_bytes(c->K);
     for (int r = 0; r < kMaxXchgRanks; ++r) a->rx_peer[r] = c->rx_peer[r];
+}
+
+// The receive ring of a node-sharded rank, for every way an exchange is set up (ksched_xchg_export,
+// ksched_xchg_join_local_ex): (re)allocated when its size or memory kind changes, and ZEROED AT EVERY SETUP, in
+// this context's stream order and finished, before any peer can learn where it is.  So a ring never holds a
+// granule of an earlier setup, and every setup's epochs start at 1 (tag 0 is never live) -- the one epoch rule
+// of both paths.  Uncached (hipDeviceMallocUncached): a peer GPU's xGMI stores and this GPU's polls meet in
+// memory, never in a stale L2 line.
+int rx_prepare(ksched_ctx *c, size_t bytes, bool uncached) {
+    if (c->d_rx && (c->rx_bytes < bytes || c->rx_uncached != uncached)) {
+        hipFree(c->d_rx);
+        c->d_rx = nullptr;
+        c->rx_bytes = 0;
+    }
+    if (!c->d_rx) {
+        if (uncached) HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
+        else HIPCHK(c, hipMalloc(&c->d_rx, bytes));
+        c->rx_bytes = bytes;
+        c->rx_uncached = uncached;
+    }
+    // zeroed by system-scope stores, the granules' own path (a hipMemsetAsync of an uncached ring was not what the
+    // persistent kernel's system-scope loads read afterwards: the round-4 failure)
+    HIPCHK(c, launch_zero_sys(c->d_rx, c->rx_bytes, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return KSCHED_OK;
+}
+
+// The first granule tag no ring of this process has used yet.  Every setup starts its tags at (at least) this
+// value on every rank, and every call moves it past the tags it used, so a tag never repeats in this process's
+// memory: a granule left in memory that a new ring reuses can never carry a tag the new setup waits for, even
+// where zeroing the ring did not reach what its loads read.
+std::atomic<uint32_t> g_epoch_next{1};
+void epoch_used_below(uint32_t e) {
+    uint32_t cur = g_epoch_next.load();
+    while (cur < e && !g_epoch_next.compare_exchange_weak(cur, e)) {}
+}
+
+// forget every peer ring this context mapped (IPC maps are closed; a local group's peers are plain pointers)
+void rx_unmap_peers(ksched_ctx *c) {
+    for (int r = 0; r < kMaxXchgRanks; ++r) {
+        if (c->rx_ipc[r] && c->rx_peer[r]) hipIpcCloseMemHandle(c->rx_peer[r]);
+        c->rx_peer[r] = nullptr;
+        c->rx_ipc[r] = false;
+    }
+}
+
+// rank r's ring as this context maps it from its IPC handle (ksched_xchg_import, and the local group's IPC mode)
+int rx_map_peer(ksched_ctx *c, int r, const uint8_t *handle) {
+    hipIpcMemHandle_t h;
+    static_assert(sizeof(hipIpcMemHandle_t) + 8 <= KSCHED_XCHG_HANDLE_BYTES, "ipc handle + epoch hint");
+    std::memcpy(&h, handle, sizeof(h));
+    void *p = nullptr;
+    HIPCHK(c, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    c->rx_peer[r] = static_cast<char *>(p);
+    c->rx_ipc[r] = true;
+    return KSCHED_OK;
 }
 
 // fast53 for this call: every |alloc| + sum of |requests| < 2^52, on every rank.
@@ -683,7 +741,13 @@ int enqueue_persistent(ksched_ctx *c) {
     // CUs (one workgroup per CU: k_pipe's LDS admits one, checked against the occupancy query below), whole
     // XCDs' worth (multiples of 8), one CU per XCD left over as a margin
     const ksched_lgroup *lgp = c->xchg_run ? c->lg.get() : nullptr;
-    const int share = lgp ? (c->cus - kXcds) / lgp->R / kXcds * kXcds : c->cus;
+    // (up to 4 ranks whole XCDs each; 5..8 ranks (31 CUs each on MI355X) are not rounded: whole XCDs would leave
+    // 24 CUs per rank, too few for a batch of 32's merger workgroups beside the score workgroups)
+    int share = c->cus;
+    if (lgp) {
+        share = (c->cus - kXcds) / lgp->R;
+        if (lgp->R <= 4) share = share / kXcds * kXcds;
+    }
     const int wgs = std::min(share, c->o.pipe_wgs > 0 ? c->o.pipe_wgs : c->cus);
     // merger workgroups: kPipeMergeSlots pods each, one slot per pod of a batch
     const int M = (B + kPipeMergeSlots - 1) / kPipeMergeSlots;
@@ -710,12 +774,15 @@ int enqueue_persistent(ksched_ctx *c) {
     if (info.lds + info.static_lds > 160 * 1024) return 1;  // the rows do not fit: the stream pipeline
     if (lgp && (info.occ < 1 || (int64_t)lgp->R * (kCommitWGs + G + M) > (int64_t)(c->cus - kXcds) * info.occ))
         return fail(c, KSCHED_E_INVALID, "local rank group: the ranks' grids do not fit the device together");
+    // KSCHED_PLAIN_LAUNCH (profiled runs) has no runtime residency check: the same one made here
+    if (!lgp && c->diag.plain_launch && (info.occ < 1 || (int64_t)(kCommitWGs + G + M) > (int64_t)c->cus * info.occ))
+        return 1;
     // workspace: part lists [kPipeLag][B][G][KC] with the counts in entry 0's pad (score(b + kPipeLag) reuses
     // batch b's), list ring 4 x (B*K Rec + B fc), XBuf ring
     const size_t part_b = align_up((size_t)kPipeLag * B * G * KC * sizeof(Cand), 256);
     const size_t cnt_b = 0;
     const size_t lists_b = align_up((size_t)B * K * sizeof(Rec) + (size_t)B * sizeof(int64_t), 256);
-    const size_t xb = align_up(xbuf_bytes(B), 256);
+    const size_t xb = align_up(xbuf_bytes_pipe(B), 256);
     const size_t prog_b = align_up((size_t)(G + B + kCommitWGs) * kProgWords * 8, 256);
     const size_t resc_b = align_up(rescue_bytes(B), 256);
     const size_t inh_b = align_up(inh_bytes(B), 256);
@@ -738,8 +805,9 @@ int enqueue_persistent(ksched_ctx *c) {
     a.xring = a.lring + 4 * lists_b;
     a.xbuf_bytes = (int64_t)xb;
     a.prog = reinterpret_cast<uint64_t *>(a.xring + 5 * xb);
-    // the rescue of exhausted lists needs the whole node set on this device: one rank only (R > 1 truncates)
-    a.rescue = c->xchg_run || c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
+    // the rescue of exhausted lists: each rank's merger slots scan its own shard, node-sharded ranks fold their
+    // results through the rings (ksched_commit.h rescue_rank_fold)
+    a.rescue = c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     a.rescue_max = c->diag.rescue_max;
     a.inh = reinterpret_cast<char *>(a.prog) + prog_b + resc_b;
     c->d_prog = a.prog;
@@ -795,7 +863,8 @@ int enqueue_persistent(ksched_ctx *c) {
         a.poison_lds = (int32_t)info.lds;
     }
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
-    for (int r = 0; r < 5; ++r) HIPCHK(c, hipMemsetAsync(a.xring + (size_t)r * xb, 0, 8, sS));
+    // the export ring whole: its records carry batch tags (store_xrec), which an earlier call's must never match
+    HIPCHK(c, hipMemsetAsync(a.xring, 0, 5 * xb, sS));
     HIPCHK(c, hipMemsetAsync(a.prog, 0, (size_t)(G + B + kCommitWGs) * kProgWords * 8, sS));
     // score -> merge records carry 16-bit batch tags (1 + batch): no record of an earlier call may look current
     HIPCHK(c, hipMemsetAsync(a.part, 0, part_b, sS));
@@ -1003,8 +1072,7 @@ int ksched_destroy(ksched_ctx *c) {
     for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
     hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_trace_wg); hipFree(c->d_xmin);
-    for (int r = 0; r < kMaxXchgRanks; ++r)  // a local group's peers are its own contexts' rings, not IPC maps
-        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[r]);
+    rx_unmap_peers(c);
     c->lg.reset();
     hipFree(c->d_rx);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -1080,53 +1148,63 @@ int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) 
     if (c->group) return fail(c, KSCHED_E_STATE, "xchg_export: context uses an in-process rank group");
     if (c->lg) return fail(c, KSCHED_E_STATE, "xchg_export: context is in a local rank group (xchg_join_local)");
     HIPCHK(c, hipSetDevice(c->dev));
-    const size_t bytes = xchg_ring_bytes(R, c->B, c->K);
-    if (!c->d_rx) {
-        // uncached: a peer's xGMI stores and this GPU's polls meet in memory, never in a stale L2 line
-        HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
-        // tag 0 is never a live tag (epochs start at 1); zeroed in the stream order of this context's kernels
-        HIPCHK(c, hipMemsetAsync(c->d_rx, 0, bytes, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->rx_bytes = bytes;
-    }
+    // a re-export (a second setup_exchange) drops this rank's maps of the old peers before its ring is zeroed
+    rx_unmap_peers(c);
+    c->xchg_ready = false;
+    if (int rc = rx_prepare(c, xchg_ring_bytes(R, c->B, c->K), true); rc != KSCHED_OK) return rc;
     if (!c->d_xmin) HIPCHK(c, hipMalloc((void **)&c->d_xmin, sizeof(int32_t)));
     hipIpcMemHandle_t h;
     HIPCHK(c, hipIpcGetMemHandle(&h, c->d_rx));
-    static_assert(sizeof(hipIpcMemHandle_t) == KSCHED_XCHG_HANDLE_BYTES, "ipc handle size");
+    // the blob: the IPC handle, then this process's first unused granule tag (the setup's tags start at the
+    // largest hint of all ranks)
+    std::memset(handle, 0, KSCHED_XCHG_HANDLE_BYTES);
     std::memcpy(handle, &h, sizeof(h));
+    const uint32_t hint = g_epoch_next.load();
+    std::memcpy(handle + sizeof(h), &hint, sizeof(hint));
     return KSCHED_OK;
 }
 
 int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
     if (!c || !handles) return KSCHED_E_INVALID;
     if (!c->d_rx) return fail(c, KSCHED_E_STATE, "xchg_import before xchg_export");
+    if (c->lg) return fail(c, KSCHED_E_STATE, "xchg_import: context is in a local rank group (xchg_join_local)");
     HIPCHK(c, hipSetDevice(c->dev));
     const int R = c->o.nranks;
-    for (int r = 0; r < kMaxXchgRanks; ++r) {
-        if (c->rx_peer[r] && c->rx_peer[r] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[r]);
-        c->rx_peer[r] = nullptr;
-    }
-    c->lg.reset();
+    rx_unmap_peers(c);
     c->xchg_ready = false;
     for (int r = 0; r < R; ++r) {
         if (r == c->o.rank) { c->rx_peer[r] = static_cast<char *>(c->d_rx); continue; }
-        hipIpcMemHandle_t h;
-        std::memcpy(&h, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES, sizeof(h));
-        void *p = nullptr;
-        HIPCHK(c, hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-        c->rx_peer[r] = static_cast<char *>(p);
+        if (int rc = rx_map_peer(c, r, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES); rc != KSCHED_OK) {
+            rx_unmap_peers(c);
+            return rc;
+        }
     }
+    // every ring was zeroed by its rank's export of this setup, before its handle left (rx_prepare), AND the tags
+    // start at the largest hint of all ranks: beyond any tag any of their processes used, so no granule left in
+    // reused memory can match (the same R blobs on every rank: the same epoch on every rank)
+    uint32_t e0 = 1;
+    for (int r = 0; r < R; ++r) {
+        uint32_t hint = 0;
+        std::memcpy(&hint, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES + sizeof(hipIpcMemHandle_t), sizeof(hint));
+        e0 = std::max(e0, hint);
+    }
+    epoch_used_below(e0 + 1);
     c->xchg_ready = true;
-    c->xchg_epoch = 1;
+    c->xchg_epoch = e0;
     return KSCHED_OK;
 }
 
 int ksched_xchg_ready(const ksched_ctx *c) { return c && c->xchg_ready ? 1 : 0; }
 
-int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) {
+int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) { return ksched_xchg_join_local_ex(ctxs, n, 0); }
+
+int ksched_xchg_join_local_ex(ksched_ctx *const *ctxs, int32_t n, int32_t flags) {
     if (!ctxs || n < 2 || n > kMaxLocalRanks) return KSCHED_E_INVALID;
+    if (flags & ~(KSCHED_XCHG_RINGS_UNCACHED | KSCHED_XCHG_RINGS_IPC)) return KSCHED_E_INVALID;
     for (int r = 0; r < n; ++r)
         if (!ctxs[r]) return KSCHED_E_INVALID;
+    const bool ipc = (flags & KSCHED_XCHG_RINGS_IPC) != 0;
+    const bool uncached = ipc || (flags & KSCHED_XCHG_RINGS_UNCACHED) != 0;
     ksched_ctx *c0 = ctxs[0];
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
@@ -1145,35 +1223,44 @@ int ksched_xchg_join_local(ksched_ctx *const *ctxs, int32_t n) {
     HIPCHK(c0, hipSetDevice(c0->dev));
     for (int r = 0; r < n; ++r) HIPCHK(c0, hipEventCreateWithFlags(&g->ready[r], hipEventDisableTiming));
     HIPCHK(c0, hipEventCreateWithFlags(&g->done, hipEventDisableTiming));
-    const size_t bytes = xchg_ring_bytes(n, c0->B, c0->K);
+    // every ring through rx_prepare, as xchg_export's: (re)allocated, zeroed at this setup and finished before
+    // any rank of the group can see it.  Plain device memory by default (one device, one kernel: the granules
+    // are sc1 traffic inside one device's memory, like the score -> merge records); uncached as export's on request
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
-        if (c->d_rx && c->rx_bytes < bytes) { hipFree(c->d_rx); c->d_rx = nullptr; }
-        if (!c->d_rx) {
-            // one device, one kernel: the granules are sc1 traffic inside one device's memory (like the score
-            // -> merge lists), so plain device memory serves; xchg_export's rings are uncached because a peer
-            // GPU's xGMI stores and this GPU's polls must meet in memory
-            HIPCHK(c, hipMalloc(&c->d_rx, bytes));
-            c->rx_bytes = bytes;
-        }
-        // zeroed in the context's stream order (its kernels run on non-blocking streams, which a legacy-stream
-        // hipMemset does not order), and finished before anyone launches
-        HIPCHK(c, hipMemsetAsync(c->d_rx, 0, c->rx_bytes, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        rx_unmap_peers(c);
+        c->lg.reset();
+        c->xchg_ready = false;
+        if (int rc = rx_prepare(c, xchg_ring_bytes(n, c0->B, c0->K), uncached); rc != KSCHED_OK) return rc;
     }
-    // granule tags of this group start at a base no earlier group of this process used: a ring allocated where
-    // an earlier group's ring was can never hold a granule whose tag this group waits for
-    static std::atomic<uint32_t> epoch_bases{0};
-    const uint32_t epoch0 = (epoch_bases.fetch_add(1) + 1u) << 20;
+    std::vector<uint8_t> handles;
+    if (ipc) {  // the multi-process path's handles: each ring exported, every peer's opened from its handle
+        handles.resize((size_t)n * KSCHED_XCHG_HANDLE_BYTES);
+        for (int r = 0; r < n; ++r) {
+            hipIpcMemHandle_t h;
+            HIPCHK(ctxs[r], hipIpcGetMemHandle(&h, ctxs[r]->d_rx));
+            std::memcpy(handles.data() + (size_t)r * KSCHED_XCHG_HANDLE_BYTES, &h, sizeof(h));
+        }
+    }
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
-        for (int q = 0; q < kMaxXchgRanks; ++q) {
-            if (c->rx_peer[q] && c->rx_peer[q] != c->d_rx && !c->lg) hipIpcCloseMemHandle(c->rx_peer[q]);
-            c->rx_peer[q] = q < n ? static_cast<char *>(ctxs[q]->d_rx) : nullptr;
+        for (int q = 0; q < n; ++q) {
+            if (q == r || !ipc) {
+                c->rx_peer[q] = static_cast<char *>(ctxs[q]->d_rx);
+            } else if (int rc = rx_map_peer(c, q, handles.data() + (size_t)q * KSCHED_XCHG_HANDLE_BYTES); rc != KSCHED_OK) {
+                for (int u = 0; u <= r; ++u) rx_unmap_peers(ctxs[u]);
+                return rc;
+            }
         }
+    }
+    // the same epoch rule as xchg_import: the process's first unused tag (one process: one hint)
+    const uint32_t e0 = std::max<uint32_t>(1u, g_epoch_next.load());
+    epoch_used_below(e0 + 1);
+    for (int r = 0; r < n; ++r) {
+        ksched_ctx *c = ctxs[r];
         c->lg = g;
         c->xchg_ready = true;
-        c->xchg_epoch = epoch0;
+        c->xchg_epoch = e0;
     }
     return KSCHED_OK;
 }
@@ -1182,6 +1269,7 @@ int ksched_xchg_close(ksched_ctx *c) {
     if (!c) return KSCHED_E_INVALID;
     c->xchg_ready = false;
     c->xchg_run = false;
+    rx_unmap_peers(c);  // the peers' rings are no longer used (IPC maps closed); the own ring stays allocated
     return KSCHED_OK;
 }
 
@@ -1660,9 +1748,11 @@ static int sync_impl(ksched_ctx *c) {
     int32_t e = 0;
     HIPCHK(c, hipMemcpy(&e, c->d_err, sizeof(e), hipMemcpyDeviceToHost));
     if (c->xchg_run) {
-        // every rank counted the same active batches: the next call's tags start past this call's
+        // every rank counted the same active batches and rescues (batch tags epoch0 + a, rescue tags epoch0 + q):
+        // the next call's tags start past this call's, and this process never uses them again
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
-        c->xchg_epoch += (uint32_t)h->nact + 2u;
+        c->xchg_epoch += (uint32_t)h->nact + (uint32_t)h->stats[4] + 2u;
+        epoch_used_below(c->xchg_epoch);
         if (e) c->xchg_ready = false;  // the rings' state is unknown: later calls take the RCCL path
         c->xchg_run = false;
     }

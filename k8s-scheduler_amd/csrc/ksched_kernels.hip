@@ -2,6 +2,8 @@
 // -ffp-contract=off: every double op rounds individually, exactly like the Go reference.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ksched_kernels.h"
 #include "ksched_merge.h"
 
@@ -1134,6 +1136,19 @@ hipError_t launch_explain(const NodeRec *nodes, int64_t n, int64_t rc, int64_t r
 
 hipError_t launch_ctl_init(Ctl *ctl, int B, int64_t P, int lag, hipStream_t s) {
     hipLaunchKernelGGL(k_ctl_init, dim3(1), dim3(64), 0, s, ctl, B, P, lag);
+    return hipGetLastError();
+}
+
+__global__ void k_zero_sys(uint64_t *p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        __hip_atomic_store(p + i, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_zero_sys(void *p, size_t bytes, hipStream_t s) {
+    const int64_t n = (int64_t)(bytes / 8);
+    if (n <= 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_zero_sys, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<uint64_t *>(p), n);
     return hipGetLastError();
 }
 

@@ -377,7 +377,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     // state there, sc1).  The caller has seen commit(bb - kPipeLag) published (stop: it timed out instead).
     auto load_apply = [&](int64_t bb, int stop, int64_t *p0v, int64_t *donev, int *errv) {
         int nxv = 0;
-        u32x4 x0 = {0u, 0u, 0u, 0u}, x1 = {0u, 0u, 0u, 0u};  // entry chunks {idx, pad, cur0} {cur1, cur2}
+        // entry chunks {tag, idx, cur0} {tag, cur1, cur2.lo} {tag, cur2.hi, -} (store_xrec's persistent layout)
+        u32x4 x0 = {0u, 0u, 0u, 0u}, x1 = {0u, 0u, 0u, 0u}, x2 = {0u, 0u, 0u, 0u};
         const XBuf *xb =
             reinterpret_cast<const XBuf *>(P.xring + (size_t)((bb >= kPipeLag ? bb - kPipeLag : 0) % 4) * P.xbuf_bytes);
         if (lane == 0) {
@@ -393,26 +394,25 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             nxv = (uint32_t)(hdr >> 32) == (uint32_t)(bb - kPipeLag) ? (int)(uint32_t)hdr : 0;
             if (lane < 2 * P.B) {                      // speculative: entries past the count are ignored
                 const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);  // uniform base, the lane's entry by offset
-                const uint32_t o = (uint32_t)lane * (uint32_t)sizeof(XRec);
-                x0 = ld_coh16(rs, o); x1 = ld_coh16(rs, o + 16);
+                const uint32_t o = (uint32_t)lane * kXRecPipe;
+                x0 = ld_coh16(rs, o); x1 = ld_coh16(rs, o + 16); x2 = ld_coh16(rs, o + 32);
             }
         }
-        auto apply = [&](const u32x4 &c0, const u32x4 &c1) {
-            const int64_t j = (int64_t)(int32_t)c0.x - P.node_offset;  // local row
+        auto apply = [&](const u32x4 &c0, const u32x4 &c1, const u32x4 &c2) {
+            const int64_t j = (int64_t)(int32_t)c0.y - P.node_offset;  // local row
             if (j < 0 || j >= n || j % G != g) return;  // another rank's node, or another workgroup's
-            const int64_t a0 = (int64_t)(((uint64_t)c0.w << 32) | c0.z), a1 = (int64_t)(((uint64_t)c1.y << 32) | c1.x),
-                          a2 = (int64_t)(((uint64_t)c1.w << 32) | c1.z);
+            const int64_t a0 = w64(c0.z, c0.w), a1 = w64(c1.y, c1.z), a2 = w64(c1.w, c2.y);
             set_row(rows + j / G, a0, a1, a2);
             if (P.screen_ok) ysq[j / G] = make_float4(screen_recip(a0), screen_recip(a1), screen_recip(a2), 0.0f);
             st_coh(&P.nodes[j].a[0], (uint64_t)a0);
             st_coh(&P.nodes[j].a[1], (uint64_t)a1);
             st_coh(&P.nodes[j].a[2], (uint64_t)a2);
         };
-        if (lane < nxv) apply(x0, x1);
+        if (lane < nxv) apply(x0, x1, x2);
         for (int e = 64 + lane; e < nxv; e += 64) {  // exports beyond 64 entries (B > 64 only)
             const __amdgpu_buffer_rsrc_t rs = coh_rsrc(xb->e);
-            const uint32_t o = (uint32_t)e * (uint32_t)sizeof(XRec);
-            apply(ld_coh16(rs, o), ld_coh16(rs, o + 16));
+            const uint32_t o = (uint32_t)e * kXRecPipe;
+            apply(ld_coh16(rs, o), ld_coh16(rs, o + 16), ld_coh16(rs, o + 32));
         }
     };
     for (int64_t b = 0;; ++b) {
@@ -808,6 +808,9 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         if (g == 0 && tid == 0) trace_at(P, b, 10);
         const size_t part_elems = (size_t)P.B * G;
         Cand *part = P.part + (size_t)(b % kPipeLag) * part_elems * KC;  // merge(b) is done before score(b + kPipeLag)
+        // Wave 0's export apply (the node rows the mergers read for the candidates' state) complete before the
+        // arrival: drained here, a whole scan after it was issued (free by now), independent of what follows
+        if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (folds && pl < P.B && p0 + pl < NP && src < KC) {
             // every lane of the group holds the pod's list: lane src stores entry src as one 16-B record
             // {key, idx, pad}, entry 0's pad carrying the workgroup's predicate count for the pod
@@ -824,10 +827,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, tag | (src == 0 ? (uint32_t)s_cnt[pl] : 0u)};
             st_coh16(coh_rsrc(part), (uint32_t)((((size_t)pl * G + g) * KC + src) * sizeof(Cand)), v);
         }
-        // The records need no drain (the mergers read them again until their tags are this batch's); what does is
-        // wave 0's export apply, the node rows the mergers read for the candidates' state: every vector memory
-        // operation of wave 0 but its newest -- the record store -- complete
-        if (wave == 0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        // The records need no drain (the mergers read them again until their tags are this batch's)
         sync();  // every wave's record stores issued
         if (wave == 0) {
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
@@ -1209,7 +1209,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
     __syncthreads();
     const int64_t cursor0 = loc.cursor;
     const int cslot = P.G + P.B + par;  // progress slot
-    constexpr int kPoller = 128;  // wave 2 lane 0: its wave loads nothing else in the prologue
+    constexpr int kPoller = 128;  // the merges' wait: wave 2 lane 0 (its wave loads nothing else in the prologue)
     const int rep = (par + kCtlReplicas - 1) % kCtlReplicas;  // the committed replica this workgroup polls
     int64_t nact = 0;  // active batches among 0 .. b (both workgroups' batches)
     int idle = 0;
@@ -1263,43 +1263,58 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
             if (threadIdx.x == 0) trace_at(P, b, 3);
             return true;
         };
-        // commit(b - 1) -> commit(b): the two hand-off granules tagged b (Ctl::hrec, put_handoff) -- or the end of
-        // the call (Ctl::committed >= 2^62: the last pod resolved, or an error elsewhere)
-        auto handoff = [&](HandoffRes *r) -> int {
-            if (threadIdx.x == kPoller) {
+        // commit(b - 1) -> commit(b): the two hand-off granules tagged b (Ctl::hrec, put_handoff) and the n1 entries of
+        // export(b - 1), every 16-byte chunk tagged b (store_xrec), polled together by wave 0 (lane = entry) -- one
+        // round of loads shows the record and the export, and commit(b - 1) drains nothing in front of them -- or the
+        // end of the call (Ctl::committed >= 2^62: the last pod resolved, or an error elsewhere)
+        const XRec *xin_e = reinterpret_cast<const XBuf *>(P.xring + (size_t)(b >= 1 ? (b - 1) % 4 : 4) * P.xbuf_bytes)->e;
+        auto handoff = [&](HandoffRes *r, XRec *xo) -> int {
+            if (threadIdx.x < 64) {
+                const int lane = (int)threadIdx.x;
                 int st = 0;
                 HandoffRes h{};
                 if (b == 0) {
                     h.cursor = cursor0;
                     h.plan_next = (int64_t)ld_coh(&ctl->plan[(kPipeLag - 1) % kPlanRing]);
                 } else {
-                    prog_at(P, cslot, b, kProgWaitCommit, 0);
+                    if (lane == 0) prog_at(P, cslot, b, kProgWaitCommit, 0);
                     const __amdgpu_buffer_rsrc_t hr = coh_rsrc(&ctl->hrec);
+                    const uint32_t tag = (uint32_t)b;
                     const uint64_t t0 = wall_clock64();
                     for (int it = 1;; ++it) {
-                        const u32x4 c0 = ld_coh16(hr, 0), c1 = ld_coh16(hr, 16);
-                        if (c0.x == (uint32_t)b && c1.x == (uint32_t)b) {
-                            h.n1 = (int32_t)c0.y;
+                        const u32x4 c0 = ld_coh16(hr, 0), c1 = ld_coh16(hr, 16);  // one address: one request
+                        const bool eok = load_xrec_pipe(xin_e, lane, tag, xo);
+                        const bool hok = __builtin_amdgcn_readfirstlane((int)(c0.x == tag && c1.x == tag)) != 0;
+                        const int n1 = hok ? (int)__builtin_amdgcn_readfirstlane((int)c0.y) : 64;
+                        if (hok && __ballot(lane < n1 && !eok) == 0) {
+                            h.n1 = n1;
                             h.cursor = (int64_t)((uint64_t)c0.w << 32 | c0.z);
                             h.rseq = (int64_t)c1.y;
                             h.plan_next = (int64_t)((uint64_t)c1.w << 32 | c1.z);
                             break;
                         }
                         if ((it & 63) == 0) {
-                            const unsigned long long cm =
-                                __hip_atomic_load(&ctl->committed_x[rep].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            if (cm >= (1ull << 62)) { st = 1; break; }
-                            if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) {
-                                prog_at(P, cslot, b, kProgWaitCommit | kProgTimedOut, cm);
-                                st = -1;
-                                break;
+                            int end = 0;
+                            if (lane == 0) {
+                                const unsigned long long cm =
+                                    __hip_atomic_load(&ctl->committed_x[rep].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                if (cm >= (1ull << 62)) {
+                                    end = 1;
+                                } else if ((int64_t)(wall_clock64() - t0) > P.timeout_ticks) {
+                                    prog_at(P, cslot, b, kProgWaitCommit | kProgTimedOut, cm);
+                                    end = -1;
+                                }
                             }
+                            end = __builtin_amdgcn_readfirstlane(end);
+                            if (end) { st = end; break; }
                         }
                         __builtin_amdgcn_s_sleep(1);
                     }
                 }
-                s_ho = h;
-                s_hr = st;
+                if (lane == 0) {
+                    s_ho = h;
+                    s_hr = st;
+                }
             }
             __syncthreads();
             *r = s_ho;
@@ -1324,7 +1339,8 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         ca.dbg = P.cdbg;
         ca.trace_row = (P.trace && b < P.trace_cap) ? P.trace + b * kTraceCols : nullptr;
         ca.loc = &loc;
-        ca.rescue = P.rescue;  // null for R > 1: an exhausted list truncates its batch there
+        ca.rescue = P.rescue;  // null: an exhausted list truncates its batch (KSCHED_RESCUE_MAX=0)
+        ca.xp = &P;            // R > 1: the rescue's rank fold
         ca.rescue_n = P.B;
         ca.rescue_max = P.rescue_max;
         ca.inh = P.inh;

@@ -23,14 +23,15 @@ E_UNKNOWN_NODE = -6
 NO_FIT = -1
 NO_POSITIVE_SCORE = -2
 
-ABI_VERSION = 5
+ABI_VERSION = 6
+XCHG_RINGS_UNCACHED, XCHG_RINGS_IPC = 1, 2
 MODE_EXACT, MODE_BATCHED, MODE_AUTO = 0, 1, 2
 PIPELINE_AUTO, PIPELINE_STREAM = 0, 1
 PRIORITY_RESOURCE, PRIORITY_BEST_PRICE = 0, 1
 DOMAIN_ALL, DOMAIN_FEASIBLE = 0, 1
 REASON_FIT, REASON_CPU, REASON_MEMORY, REASON_POD, REASON_LABELS = 0, 1, 2, 3, 4
 NUM_REASONS = 5
-XCHG_HANDLE_BYTES = 64
+XCHG_HANDLE_BYTES = 128
 # the reference's per-node failure text (anchor/predicate.go:135,140,145)
 REASON_TEXT = {REASON_CPU: "Insufficient CPU", REASON_MEMORY: "Insufficient Memory", REASON_POD: "Insufficient Pod",
                REASON_LABELS: "node labels do not match the pod's selector"}
@@ -89,6 +90,7 @@ SIGNATURES = [
     ("ksched_xchg_ready", C.c_int, [CTX]),
     ("ksched_xchg_close", C.c_int, [CTX]),
     ("ksched_xchg_join_local", C.c_int, [C.POINTER(CTX), C.c_int32]),
+    ("ksched_xchg_join_local_ex", C.c_int, [C.POINTER(CTX), C.c_int32, C.c_int32]),
     ("ksched_load_nodes", C.c_int, [CTX, C.c_int64, I64P, I64P, I64P, U64P, F32P]),
     ("ksched_apply_delta", C.c_int, [CTX, C.c_int64, I32P, I64P, I64P, I64P]),
     ("ksched_explain", C.c_int, [CTX, C.c_int64, C.c_int64, C.c_int64, C.c_uint64, I64P, C.POINTER(C.c_uint8)]),
@@ -123,11 +125,16 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C {PKG_ROOT}` (no CPU fallback exists)")
         lb = C.CDLL(LIB_PATH)
+        # KSCHED_LIB (a same-box A/B against an older build, tools/build_base.sh) admits the previous ABI: entry
+        # points it lacks stay unbound (calling one raises AttributeError)
+        ab = bool(os.environ.get("KSCHED_LIB"))
         for name, res, args in SIGNATURES:
+            if ab and not hasattr(lb, name):
+                continue
             fn = getattr(lb, name)
             fn.restype = res
             fn.argtypes = args
-        if lb.ksched_abi_version() != ABI_VERSION:
+        if lb.ksched_abi_version() != ABI_VERSION and not (ab and lb.ksched_abi_version() >= ABI_VERSION - 1):
             raise ImportError("libksched ABI version mismatch")
         _lib = lb
     return _lib

@@ -8,7 +8,7 @@ identically, and replay the same ordered commit -- each rank writes back only th
 Two exchange transports: the persistent pipeline's device-side exchange (ksched_xchg_*: merger
 workgroups write every pod's list straight into each rank's receive ring over xGMI, no launch per
 batch), or one RCCL all-gather per batch in the stream pipeline.  torch.distributed only hands out
-the 128-byte RCCL unique id and the 64-byte IPC handles of the rings.
+the 128-byte RCCL unique id and the 128-byte ring handles (IPC handle + epoch hint).
 """
 from __future__ import annotations
 
@@ -110,14 +110,15 @@ def gather_node_state(local_state, world: int):
     return tuple(out)
 
 
-def make_local_xchg_group(cl, world: int, device: int = 0, **kw):
+def make_local_xchg_group(cl, world: int, device: int = 0, rings: str = "plain", **kw):
     """`world` node-sharded ranks of cluster `cl` as contexts of THIS process on ONE device, joined by the
-    device-side exchange without IPC (ksched_xchg_join_local): their persistent kernels run as one
-    cooperative launch, so all ranks' grids are resident at once.  The caller runs each rank's schedule
-    calls in its own thread.  Returns [(engine, (lo, hi)) per rank]."""
+    device-side exchange (ksched_xchg_join_local_ex; rings: "plain", "uncached" = xchg_export's ring kind, "ipc" =
+    also mapped through IPC handles): their persistent kernels run as one cooperative launch, so all ranks'
+    grids are resident at once.  The caller runs each rank's schedule calls in its own thread.  Returns
+    [(engine, (lo, hi)) per rank]."""
     from . import _lib as L
     from .engine import Engine
     out = [make_sharded_engine(cl, r, world, device=device, mode=L.MODE_BATCHED, comm=False, **kw)
            for r in range(world)]
-    Engine.xchg_join_local([e for e, _ in out])
+    Engine.xchg_join_local([e for e, _ in out], rings=rings)
     return out

@@ -118,11 +118,23 @@ class Engine:
         self._chk(L.lib().ksched_xchg_close(self._ctx), "xchg_close")
 
     @staticmethod
-    def xchg_join_local(engines):
-        """Ranks as threads of this process on one device (engines[r] = rank r): the device exchange without
-        IPC, the ranks' persistent kernels as ONE cooperative launch (ksched_xchg_join_local)."""
+    def xchg_join_local(engines, rings: str = "plain"):
+        """Ranks as threads of this process on one device (engines[r] = rank r): the device exchange, the ranks'
+        persistent kernels as ONE cooperative launch (ksched_xchg_join_local_ex).  rings: "plain" device memory,
+        "uncached" (allocated, zeroed and tagged exactly as xchg_export's) or "ipc" (uncached, and every peer's
+        ring mapped from its IPC handle as xchg_import does)."""
+        flags = {"plain": 0, "uncached": L.XCHG_RINGS_UNCACHED, "ipc": L.XCHG_RINGS_IPC}[rings]
         arr = (L.CTX * len(engines))(*[e._ctx for e in engines])
-        L.check(L.lib().ksched_xchg_join_local(arr, len(engines)), engines[0]._ctx, "xchg_join_local")
+        L.check(L.lib().ksched_xchg_join_local_ex(arr, len(engines), flags), engines[0]._ctx, "xchg_join_local")
+
+    @staticmethod
+    def close_group(engines):
+        """Close the ranks of a local group: every rank's peer maps first (xchg_close), then the contexts."""
+        for e in engines:
+            if e._ctx:
+                L.lib().ksched_xchg_close(e._ctx)
+        for e in engines:
+            e.close()
 
     @property
     def xchg_ready(self) -> bool:

@@ -564,8 +564,33 @@ typedef struct or_rescue {
     const int64_t *ac, *am, *ap;
     const uint64_t *labels;
     const float *price;
-    int64_t count;  /* rescues performed */
+    int64_t count;     /* rescues performed */
+    int32_t shards;    /* the node rows as R contiguous shards (ksched.dist.shard_range): each shard's best
+                          untouched node, then the best of the R (the device's node-sharded rescue); 1: one scan */
+    int32_t max_per_batch;  /* rescues a batch may make before an exhausted list truncates it (< 0: no limit;
+                               the device's KSCHED_RESCUE_MAX) */
+    int32_t in_batch;  /* rescues made by the batch being committed */
 } or_rescue;
+
+/* The best node outside the touched set (touched[0, nt)) over rows [lo, hi) at their current state; -1: none
+ * eligible.  anchor/priorities.go:45-61's loop, restricted to the untouched rows. */
+static int64_t rescue_scan(const or_opts *o, const or_rescue *rs, int64_t lo, int64_t hi, int64_t rc, int64_t rm,
+                           int64_t rp, uint64_t s, int ul, const or_touched *touched, int32_t nt, double *bk)
+{
+    int64_t j, bj = -1;
+    int32_t t;
+    for (j = lo; j < hi; j++) {
+        double k;
+        int ft, is_t = 0;
+        for (t = 0; t < nt; t++) if (touched[t].idx == j) { is_t = 1; break; }
+        if (is_t) continue;
+        ft = fits(rc, rm, rp, s, rs->ac[j], rs->am[j], rs->ap[j], ul ? rs->labels[j] : 0, ul);
+        if (!pair_key(o, ft, rc, rm, rp, rs->ac[j], rs->am[j], rs->ap[j], rs->price ? rs->price[j] : 0.f, &k))
+            continue;
+        if (bj < 0 || cand_better(k, j, *bk, bj)) { *bk = k; bj = j; }
+    }
+    return bj;
+}
 
 static int64_t commit_batch_impl(const or_opts *o, int32_t K, int64_t nb,
                                  const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
@@ -594,6 +619,7 @@ static int64_t commit_batch_impl(const or_opts *o, int32_t K, int64_t nb,
 {
     int64_t i;
     int use_labels = o->use_labels && sel;
+    if (rs) rs->in_batch = 0;
     for (i = 0; i < nb; i++) {
         const or_rec *L = lists + i * K;
         const uint64_t s = use_labels ? sel[i] : 0;
@@ -631,24 +657,23 @@ static int64_t commit_batch_impl(const or_opts *o, int32_t K, int64_t nb,
             if (tb >= 0) { w = touched[tb].idx; wkey = tkey; }
         } else {
             if (tb >= 0 && cand_better(tkey, touched[tb].idx, L[K - 1].key, L[K - 1].idx)) { w = touched[tb].idx; wkey = tkey; }
-            else if (!rs) return i; /* overflow: the best untouched node may lie beyond the list */
+            else if (!rs || (rs->max_per_batch >= 0 && rs->in_batch >= rs->max_per_batch))
+                return i; /* overflow: the best untouched node may lie beyond the list */
             else {
-                /* rescue: the best node outside the touched set over every node, at its current state */
-                int64_t j, bj = -1;
+                /* rescue: the best node outside the touched set over every node, at its current state -- per
+                 * shard (each rank scans its own rows), then the best of the shards' results */
+                int64_t bj = -1;
                 double bk = 0.0;
                 int ul = o->use_labels && rs->labels && sel;
-                for (j = 0; j < rs->n; j++) {
-                    double k;
-                    int ft, is_t = 0;
-                    for (t = 0; t < *ntouched; t++) if (touched[t].idx == j) { is_t = 1; break; }
-                    if (is_t) continue;
-                    ft = fits(rc[i], rm[i], rp[i], s, rs->ac[j], rs->am[j], rs->ap[j], ul ? rs->labels[j] : 0, ul);
-                    if (!pair_key(o, ft, rc[i], rm[i], rp[i], rs->ac[j], rs->am[j], rs->ap[j],
-                                  rs->price ? rs->price[j] : 0.f, &k))
-                        continue;
-                    if (bj < 0 || cand_better(k, j, bk, bj)) { bk = k; bj = j; }
+                int32_t r, R = rs->shards > 0 ? rs->shards : 1;
+                for (r = 0; r < R; r++) {
+                    double k = 0.0;
+                    const int64_t lo = rs->n * r / R, hi = rs->n * (r + 1) / R;
+                    const int64_t j = rescue_scan(o, rs, lo, hi, rc[i], rm[i], rp[i], s, ul, touched, *ntouched, &k);
+                    if (j >= 0 && (bj < 0 || cand_better(k, j, bk, bj))) { bk = k; bj = j; }
                 }
                 rs->count++;
+                rs->in_batch++;
                 if (tb >= 0 && (bj < 0 || cand_better(tkey, touched[tb].idx, bk, bj))) { w = touched[tb].idx; wkey = tkey; }
                 else if (bj >= 0) { w = bj; wkey = bk; rj = bj; }
             }
@@ -856,6 +881,12 @@ int or_schedule_lagged_rescue(const or_opts *o, int32_t K, int32_t B, int32_t L,
                               const uint64_t *sel, int32_t *out_idx, double *out_score, int32_t *out_feas,
                               int64_t *stats);
 
+int or_schedule_lagged_rescue2(const or_opts *o, int32_t K, int32_t B, int32_t L, int32_t rescue_max,
+                               int32_t shards, int64_t n, int64_t *ac, int64_t *am, int64_t *ap,
+                               const uint64_t *labels, const float *price, int64_t p, const int64_t *rc,
+                               const int64_t *rm, const int64_t *rp, const uint64_t *sel, int32_t *out_idx,
+                               double *out_score, int32_t *out_feas, int64_t *stats);
+
 int or_schedule_lagged(const or_opts *o, int32_t K, int32_t B, int32_t L, int64_t n,
                        int64_t *ac, int64_t *am, int64_t *ap, const uint64_t *labels, const float *price,
                        int64_t p, const int64_t *rc, const int64_t *rm, const int64_t *rp, const uint64_t *sel,
@@ -873,8 +904,22 @@ int or_schedule_lagged_rescue(const or_opts *o, int32_t K, int32_t B, int32_t L,
                               const uint64_t *sel, int32_t *out_idx, double *out_score, int32_t *out_feas,
                               int64_t *stats)
 {
+    return or_schedule_lagged_rescue2(o, K, B, L, rescue ? -1 : 0, 1, n, ac, am, ap, labels, price, p, rc, rm, rp,
+                                      sel, out_idx, out_score, out_feas, stats);
+}
+
+/* The same with the device's rescue budget and node sharding: rescue_max rescues per batch (0: none, < 0: no
+ * limit; the next exhausted list truncates the batch), the rescue's scan split over `shards` contiguous node
+ * shards whose results are folded (ksched_pipe.hip serve_rescue per rank + ksched_commit.h's rank fold). */
+int or_schedule_lagged_rescue2(const or_opts *o, int32_t K, int32_t B, int32_t L, int32_t rescue_max,
+                               int32_t shards, int64_t n, int64_t *ac, int64_t *am, int64_t *ap,
+                               const uint64_t *labels, const float *price, int64_t p, const int64_t *rc,
+                               const int64_t *rm, const int64_t *rp, const uint64_t *sel, int32_t *out_idx,
+                               double *out_score, int32_t *out_feas, int64_t *stats)
+{
     enum { RING = 8 };
-    or_rescue rs = {n, ac, am, ap, labels, price, 0};
+    or_rescue rs = {n, ac, am, ap, labels, price, 0, shards < 1 ? 1 : shards, rescue_max, 0};
+    const int rescue = rescue_max != 0;
     or_xrec *X[RING], *inh;
     int32_t nx[RING];
     int64_t plan[RING];

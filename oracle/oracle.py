@@ -169,10 +169,14 @@ def schedule_pipelined(cl, K: int, B: int, n_pods=None):
     return oi, os_, of, (ac, am, ap), dict(batches=int(st[0]), truncations=int(st[1]), skipped=int(st[2]))
 
 
-def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None, rescue: bool = False):
-    """CPU model of the persistent pipeline at lag `lag` (the device runs 3): cpu_ref.c or_schedule_lagged_rescue;
+def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None, rescue: bool = False, rescue_max=None,
+                    shards: int = 1):
+    """CPU model of the persistent pipeline at lag `lag` (the device runs 3): cpu_ref.c or_schedule_lagged_rescue2;
     rescue=True resolves an exhausted candidate list by a full scan of the untouched nodes (the device's commit)
-    instead of truncating the batch."""
+    instead of truncating the batch -- at most rescue_max per batch (None: no limit; the device's
+    KSCHED_RESCUE_MAX), the scan split over `shards` contiguous node shards whose bests are folded (the
+    node-sharded ranks' rescue)."""
+    rmax = (-1 if rescue_max is None else int(rescue_max)) if rescue else 0
     ac, am, ap = (np.ascontiguousarray(x, dtype=np.int64).copy() for x in (cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))
     p = cl.n_pods if n_pods is None else int(n_pods)
     rc, rm, rp = (np.ascontiguousarray(x[:p], dtype=np.int64) for x in (cl.req_cpu, cl.req_mem, cl.req_pods))
@@ -182,8 +186,8 @@ def schedule_lagged(cl, K: int, B: int, lag: int, n_pods=None, rescue: bool = Fa
     oi = np.empty(p, np.int32); os_ = np.empty(p, np.float64); of = np.empty(p, np.int32)
     st = np.zeros(4, np.int64)
     o = _opts(cl.priority, cl.domain, cl.use_labels)
-    r = lib().or_schedule_lagged_rescue(C.byref(o), C.c_int32(K), C.c_int32(B), C.c_int32(lag), C.c_int32(int(rescue)),
-                                        C.c_int64(ac.shape[0]),
+    r = lib().or_schedule_lagged_rescue2(C.byref(o), C.c_int32(K), C.c_int32(B), C.c_int32(lag), C.c_int32(rmax),
+                                         C.c_int32(int(shards)), C.c_int64(ac.shape[0]),
                                  _p(ac, C.c_int64), _p(am, C.c_int64), _p(ap, C.c_int64),
                                  _p(lab, C.c_uint64), _p(pr, C.c_float), C.c_int64(p),
                                  _p(rc, C.c_int64), _p(rm, C.c_int64), _p(rp, C.c_int64), _p(sel, C.c_uint64),

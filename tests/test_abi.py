@@ -31,7 +31,7 @@ def test_abi_version_and_defaults():
     import ctypes as C
     from ksched import _lib as L
     lb = L.lib()
-    assert lb.ksched_abi_version() == L.ABI_VERSION == 5
+    assert lb.ksched_abi_version() == L.ABI_VERSION == 6
     o = L.Opts()
     assert lb.ksched_default_opts(C.byref(o)) == 0
     assert o.struct_size == C.sizeof(L.Opts) and o.nranks == 1 and o.mode == L.MODE_AUTO

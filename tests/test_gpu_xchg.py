@@ -2,12 +2,15 @@
 every rank's results must equal the CPU oracle's sequential schedule, bit for bit, and the ranks' node
 shards together must equal the oracle's final state.  Exercises the product multi-rank code: global node
 indices at node_offset > 0, granule exchange through the ranks' receive rings, the rank merge in the merger
-workgroups and the owner-only write-back (the xGMI transport itself needs several GPUs).
+workgroups and the owner-only write-back.
 
-The ranks are threads of this process joined by ksched_xchg_join_local: their kernels run as ONE cooperative
+The ranks are threads of this process joined by ksched_xchg_join_local_ex: their kernels run as ONE cooperative
 launch, so every rank's grid is resident at once by construction.  (Round 3 ran them as separate processes
 with separate plain launches; one rank's kernel was once descheduled for the whole 10 s timeout -- nothing
-makes the launches of different processes co-resident.)"""
+makes the launches of different processes co-resident.)  The rings come in the three kinds the join offers:
+"plain" device memory, "uncached" -- allocated, zeroed and tagged exactly as the multi-process transport's
+ksched_xchg_export does -- and "ipc", which also maps every peer's ring through its IPC handle as
+ksched_xchg_import does.  The xGMI hop itself needs several GPUs."""
 import threading
 
 import numpy as np
@@ -16,42 +19,75 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def run_local(cl, world, calls=2):
+def run_local(cl, world, calls=2, rings="plain", batch=64, engines=None):
+    """`calls` schedule calls of cluster `cl` on `world` local ranks; returns ([per call results], final node
+    shard) per rank.  engines: an already joined group to reuse (closed by the caller)."""
     from ksched.dist import make_local_xchg_group
-    ranks = make_local_xchg_group(cl, world, device=0, topk=16, batch=64)
-    for e, (lo, hi) in ranks:
-        assert e.xchg_ready, "exchange join failed"
-        st0 = e.read_nodes()
-        assert all(np.array_equal(st0[k], a[lo:hi]) for k, a in enumerate((cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))), \
-            f"rank node state after load differs from the input (shard {lo}:{hi})"
-        e.save_state()
-    out = [None] * world
-    errs = []
+    from ksched.engine import Engine
+    own = engines is None
+    ranks = make_local_xchg_group(cl, world, device=0, topk=16, batch=batch, rings=rings) if own else engines
+    try:
+        for e, (lo, hi) in ranks:
+            assert e.xchg_ready, "exchange join failed"
+            if own:
+                st0 = e.read_nodes()
+                assert all(np.array_equal(st0[k], a[lo:hi]) for k, a in
+                           enumerate((cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods))), \
+                    f"rank node state after load differs from the input (shard {lo}:{hi})"
+                e.save_state()
+        out = [None] * world
+        errs = []
 
-    def work(r):
-        try:
-            e = ranks[r][0]
-            res = []
-            for _ in range(calls):  # repeated calls: the granule tags advance across calls
-                e.restore_state()
-                oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
-                st = e.stats()
-                res.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"],
-                            st["exact_rows"]))
-            out[r] = (res, e.read_nodes())
-        except Exception as ex:  # surfaced below
-            errs.append((r, repr(ex)))
+        def work(r):
+            try:
+                e = ranks[r][0]
+                res = []
+                for _ in range(calls):  # repeated calls: the granule tags advance across calls
+                    e.restore_state()
+                    oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods, cl.selector)
+                    st = e.stats()
+                    res.append((oi, os_.view(np.int64), of, st["pipeline"], st["batches"], st["truncations"],
+                                st["exact_rows"], st["rescues"]))
+                out[r] = (res, e.read_nodes())
+            except Exception as ex:  # surfaced below
+                errs.append((r, repr(ex)))
 
-    th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=150)
-    for e, _ in ranks:
-        e.close()
-    assert not errs, errs
-    assert all(o is not None for o in out), "a rank did not finish"
-    return out
+        th = [threading.Thread(target=work, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=150)
+        hung = [r for r, t in enumerate(th) if t.is_alive()]
+        if hung:
+            # a rank still inside schedule/sync may be running a kernel that reads its peers' rings: closing the
+            # group under it could turn a hang into a fault -- leave the contexts alone and report (ADVICE r4)
+            own = False
+            raise AssertionError(f"ranks {hung} did not finish within 150 s (group left open)")
+        assert not errs, errs
+        assert all(o is not None for o in out), "a rank did not finish"
+        return out
+    finally:
+        if own:
+            Engine.close_group([e for e, _ in ranks])
+
+
+def check_oracle(cl, out, want, world):
+    for r in range(world):
+        for c, (oi, osb, of, pipe, nb, ntr, exr, nres) in enumerate(out[r][0]):
+            assert pipe == "persistent", f"rank {r} ran the {pipe} pipeline"
+            if not np.array_equal(oi, want[0]):
+                agree = [all(np.array_equal(out[0][0][k][0], out[q][0][k][0]) for q in range(world))
+                         for k in range(len(out[0][0]))]
+                bad = np.nonzero(oi != want[0])[0][:5]
+                raise AssertionError(
+                    f"rank {r} call {c} ({nb} batches, {ntr} truncated, {exr} exact rows): assignments differ at {bad} "
+                    f"(got {oi[bad]}, oracle {want[0][bad]}; ranks agree per call: {agree}; "
+                    f"other calls: {[(x[4], x[5], x[6], int((x[0] != want[0]).sum())) for x in out[r][0]]})")
+            assert np.array_equal(osb, want[1].view(np.int64)), f"rank {r}: score bits differ"
+            assert np.array_equal(of, want[2]), f"rank {r}: feasible counts differ"
+    got = [np.concatenate([out[r][1][k] for r in range(world)]) for k in range(3)]
+    for k in range(3):
+        assert np.array_equal(got[k], want[3][k]), f"final node state (resource {k}) differs"
 
 
 @pytest.mark.parametrize("cfg,nn,pp,world", [("c3", 24000, 3000, 2), ("c5hc", 20000, 3000, 2), ("c4", 30000, 2500, 3),
@@ -60,22 +96,86 @@ def test_xchg_ranks_match_oracle(gpu_available, oracle_mod, cfg, nn, pp, world):
     from ksched import cluster
     cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
     want = oracle_mod.schedule(cl, nthreads=8)
-    out = run_local(cl, world)
-    for r in range(world):
-        for c, (oi, osb, of, pipe, nb, ntr, exr) in enumerate(out[r][0]):
-            assert pipe == "persistent", f"rank {r} ran the {pipe} pipeline"
-            if not np.array_equal(oi, want[0]):
-                w1 = oracle_mod.schedule(cl, nthreads=1)[0]
-                agree = [all(np.array_equal(out[0][0][k][0], out[q][0][k][0]) for q in range(world))
-                         for k in range(len(out[0][0]))]
-                bad = np.nonzero(oi != want[0])[0][:5]
-                raise AssertionError(
-                    f"rank {r} call {c} ({nb} batches, {ntr} truncated, {exr} exact rows): assignments differ at {bad} "
-                    f"(got {oi[bad]}, oracle {want[0][bad]}; 1-thread oracle equal to the 8-thread one: "
-                    f"{np.array_equal(w1, want[0])}; ranks agree per call: {agree}; "
-                    f"other calls: {[(x[4], x[5], x[6], int((x[0] != want[0]).sum())) for x in out[r][0]]})")
-            assert np.array_equal(osb, want[1].view(np.int64)), f"rank {r}: score bits differ"
-            assert np.array_equal(of, want[2]), f"rank {r}: feasible counts differ"
-    got = [np.concatenate([out[r][1][k] for r in range(world)]) for k in range(3)]
-    for k in range(3):
-        assert np.array_equal(got[k], want[3][k]), f"final node state (resource {k}) differs"
+    check_oracle(cl, run_local(cl, world), want, world)
+
+
+def test_xchg_eight_ranks_c4_full_nodes(gpu_available, oracle_mod):
+    """R = 8 on c4's full 100k nodes (12.5k per rank) over rings of xchg_export's kind.  Eight ranks share the
+    256 CUs (31 each): a batch of 32 (11 merger workgroups, 18 score workgroups of 695 rows per rank) fits."""
+    from ksched import cluster
+    cl = cluster.make_cluster("c4", n_nodes=100000, n_pods=3000)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    check_oracle(cl, run_local(cl, 8, rings="uncached", batch=32), want, 8)
+
+
+def test_xchg_groups_in_one_process_uncached(gpu_available, oracle_mod):
+    """Several groups in ONE process over uncached rings, in the order that failed in round 4 (two-rank groups,
+    a three-rank group, then a two-rank group whose rings can land where the earlier groups' were): each group's
+    rings are zeroed at its setup and its tags start at 1, so no group may see an earlier group's granules."""
+    from ksched import cluster
+    for cfg, nn, pp, world in (("c3", 24000, 3000, 2), ("c4", 30000, 2500, 3), ("c4", 100000, 2500, 2),
+                               ("c3", 24000, 3000, 2)):
+        cl = cluster.make_cluster(cfg, n_nodes=nn, n_pods=pp)
+        want = oracle_mod.schedule(cl, nthreads=8)
+        check_oracle(cl, run_local(cl, world, rings="uncached"), want, world)
+
+
+def test_xchg_rejoin_reuses_rings(gpu_available, oracle_mod):
+    """One group joined, run, joined AGAIN (the same contexts: the rings are reused, zeroed again and the tags
+    restart at 1 -- the rule of a second ksched_xchg_export/import) and run again: bit-exact both times."""
+    from ksched import cluster
+    from ksched.dist import make_local_xchg_group
+    from ksched.engine import Engine
+    cl = cluster.make_cluster("c4", n_nodes=60000, n_pods=2500)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    ranks = make_local_xchg_group(cl, 2, device=0, topk=16, batch=64, rings="uncached")
+    try:
+        for e, _ in ranks:
+            e.save_state()
+        check_oracle(cl, run_local(cl, 2, calls=3, engines=ranks), want, 2)
+        Engine.xchg_join_local([e for e, _ in ranks], rings="uncached")
+        check_oracle(cl, run_local(cl, 2, calls=2, engines=ranks), want, 2)
+    finally:
+        Engine.close_group([e for e, _ in ranks])
+
+
+def test_xchg_ipc_mapped_rings(gpu_available, oracle_mod):
+    """The multi-process transport's ring setup on one device: every ring allocated and zeroed as
+    ksched_xchg_export does and every peer's ring opened from its IPC handle as ksched_xchg_import does; the
+    ranks still launch as one grid.  Skipped where the runtime does not open a handle of the same process."""
+    from ksched import cluster
+    from ksched._lib import KschedError
+    cl = cluster.make_cluster("c4", n_nodes=60000, n_pods=2500)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    try:
+        out = run_local(cl, 2, rings="ipc")
+    except KschedError as ex:
+        if "hipIpcOpenMemHandle" in str(ex):
+            pytest.skip(f"same-process IPC open refused by the runtime: {ex}")
+        raise
+    check_oracle(cl, out, want, 2)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xchg_sharded_rescue(gpu_available, oracle_mod, world):
+    """Node-sharded ranks rescue exhausted candidate lists instead of truncating (each rank's mergers scan its own
+    shard, the R bests fold through the rings: ksched_commit.h rescue_rank_fold; restated by the oracle's
+    or_schedule_lagged_rescue2 with shards): bit-exact, rescues happen, and the truncations stay within 2x of one
+    rank's on the same cluster (where each rank alone would have truncated at every exhausted list)."""
+    from ksched import Engine, MODE_BATCHED, cluster
+    cl = cluster.make_cluster("c4", n_nodes=100000, n_pods=6000)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    with Engine(mode=MODE_BATCHED, priority=cl.priority, domain=cl.domain, device=0, topk=16, batch=64) as e:
+        e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods)
+        oi, _, _ = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods)
+        one = e.stats()
+    assert np.array_equal(oi, want[0])
+    out = run_local(cl, world, calls=1, rings="uncached")
+    check_oracle(cl, out, want, world)
+    st = [x for r in range(world) for x in out[r][0]]
+    resc = {x[7] for x in st}
+    trunc = {x[5] for x in st}
+    assert len(resc) == 1 and len(trunc) == 1, f"ranks disagree on rescues {resc} / truncations {trunc}"
+    nres, ntr = resc.pop(), trunc.pop()
+    assert nres > 0, f"no rescue in {world} ranks (one rank: {one['rescues']} rescues, {one['truncations']} truncated)"
+    assert ntr <= 2 * one["truncations"] + 2, f"{world} ranks truncated {ntr} batches, one rank {one['truncations']}"

@@ -232,3 +232,33 @@ def test_lagged_rescue_c4_like(oracle_mod):
     bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, 16, 64, 3, rescue=True)
     assert np.array_equal(oi, bi) and np.array_equal(of, bf) and np.array_equal(os_.view(np.int64), bs.view(np.int64))
     assert stats["truncations"] == 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_lagged_rescue_sharded_budgeted_equals_sequential(oracle_mod, seed):
+    """The node-sharded rescue (each of R contiguous shards scanned for its best untouched node, the R bests
+    folded: the device's per-rank merger scan + rank fold) under the device's per-batch budget: the sequential
+    result for every shard count and budget; the shard split changes nothing (a fold of per-shard arg-bests is
+    the arg-best), and the budget only trades rescues for truncations."""
+    from ksched import cluster
+    combos = [(0, 0, False), (0, 1, True), (1, 1, False), (0, 0, True)]
+    pr, dm, lb = combos[seed]
+    cl = cluster.random_small(191 + seed, n_nodes=97, n_pods=500, priority=pr, domain=dm, use_labels=lb)
+    oi, os_, of, st = oracle_mod.schedule(cl)
+    for K, B in ((4, 16), (8, 64)):
+        seen = {}
+        for budget in (0, 1, 4, None):
+            for shards in (1, 2, 3, 8):
+                bi, bs, bf, bst, stats = oracle_mod.schedule_lagged(cl, K, B, 3, rescue=True, rescue_max=budget,
+                                                                    shards=shards)
+                assert np.array_equal(oi, bi) and np.array_equal(of, bf)
+                assert np.array_equal(os_.view(np.int64), bs.view(np.int64))
+                for a, b in zip(st, bst):
+                    assert np.array_equal(a, b)
+                key = (stats["truncations"], stats["rescues"], stats["batches"])
+                assert seen.setdefault(budget, key) == key, "the shard count changed the schedule of rescues"
+                if budget == 0:
+                    assert stats["rescues"] == 0
+                if budget is None:
+                    assert stats["truncations"] == 0
+        assert seen[0][0] >= seen[1][0] >= seen[4][0] >= seen[None][0] == 0
