@@ -23,6 +23,10 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef KSCHED_XCHG_DEBUG
+#define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tools/xchg_ring_experiment.py (a separate build)
+#endif
+
 #include "ksched_kernels.h"
 
 namespace ksched {
@@ -155,14 +159,14 @@ struct RescueOut {
 // Node-sharded rescue (R > 1; wave 0 of the commit, o = this rank's best): every rank's commit made the same
 // request q (the ranks replay one ordered commit), and each rank's merger slots scanned only its own shard.  The
 // rank's best travels to every rank's ring -- rescue area slot (q % 2, this rank) as 14 tagged 8-byte granules
-// {word, epoch0 + q} (two parities: a rank can be one request ahead of a peer still reading the last one, never
+// (gran_enc, tag epoch0 + q; two parities: a rank can be one request ahead of a peer still reading the last one, never
 // two) -- and the R bests fold the same way on every rank (lane = source rank, (key desc, idx asc)).  Restated by
 // oracle/cpu_ref.c or_schedule_lagged_rescue2 (shards).  false: a peer's record never came (error 12).
 __device__ __forceinline__ bool rescue_rank_fold(const PersistArgs &X, unsigned long long q, int64_t timeout_ticks,
                                                  int32_t *err, RescueOut *o) {
     const int lane = threadIdx.x & 63;
     const int R = X.R;
-    const uint32_t tag = X.epoch0 + (uint32_t)q;
+    const uint32_t t16 = gran_tag(X.epoch0 + (uint32_t)q);
     const size_t off = xchg_rescue_off(R, X.B, (size_t)X.xchg_stride) +
                        ((size_t)(q & 1) * R) * kXchgRescueRec;
     Rec mine{};
@@ -175,7 +179,7 @@ __device__ __forceinline__ bool rescue_rank_fold(const PersistArgs &X, unsigned 
         uint64_t *dst = reinterpret_cast<uint64_t *>(X.rx_peer[lane] + off + (size_t)X.rank * kXchgRescueRec);
 #pragma unroll
         for (int i = 0; i < kXchgRescueWords; ++i)
-            __hip_atomic_store(dst + i, (uint64_t)mw[i] | ((uint64_t)tag << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(dst + i, gran_enc(mw[i], t16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     // lane r < R: rank r's record from this rank's own ring
     uint32_t rw[kXchgRescueWords];
@@ -185,13 +189,12 @@ __device__ __forceinline__ bool rescue_rank_fold(const PersistArgs &X, unsigned 
         const uint64_t t0 = wall_clock64();
 #pragma unroll
         for (int i = 0; i < kXchgRescueWords; ++i) {
-            uint64_t v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            while (ok && (uint32_t)(v >> 32) != tag) {
+            uint32_t wv = 0;
+            while (ok && !gran_dec(__hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), t16, &wv)) {
                 if ((int64_t)(wall_clock64() - t0) > timeout_ticks) { ok = false; break; }
                 __builtin_amdgcn_s_sleep(1);
-                v = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
-            rw[i] = (uint32_t)v;
+            rw[i] = wv;
         }
     } else {
 #pragma unroll
@@ -441,6 +444,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
 
     // ---- prologue ----
     int n1 = 0, n2 = 0, nin = 0;
+    uint64_t dbg_x1 = 0;  // diagnostics (KSCHED_XCHG_DUMP, a KSCHED_XCHG_DEBUG build)
+    (void)dbg_x1;
     const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
     const double y3 = recip(3.0);
     double *Srow = m.S + (size_t)lane * kSpcRow;
@@ -565,6 +570,18 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             const int i = tid + u * kSpcThreads;
             x2v[u] = (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) ? ld_coh_f64(x2col + i) : 0.0;
         }
+#if KSCHED_XCHG_DEBUG
+        if (A.xp && A.xp->xdbg && A.dbg_act >= 0 && A.dbg_act < A.xp->xdbg_cap) {  // diagnostics: the lists as loaded
+            uint64_t *sums = A.xp->xdbg + xdbg_sums_off(A.xp->xdbg_cap, A.xp->B, A.xp->R, K);
+#pragma unroll
+            for (int u = 0; u < kHeadPer; ++u) {
+                const int e = tid + u * kSpcThreads;
+                if (e < 64 * K && e / K < nb)
+                    atomicAdd(reinterpret_cast<unsigned long long *>(sums + ((size_t)A.dbg_act * A.xp->B + e / K) * 2 + 1),
+                              (unsigned long long)dbg_mix(w0[u], w1[u], e % K));
+            }
+        }
+#endif
         hash_lists();
 #pragma unroll
         for (int u = 0; u < kX2Per; ++u) {
@@ -594,6 +611,14 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             return 1;
         }
         n1 = ho.n1;
+#if KSCHED_XCHG_DEBUG
+        if (A.xp && A.xp->xdbg && wave == 0) {  // diagnostics: export(b - 1) as received
+            int64_t x = lane < n1 ? (int64_t)dbg_mix((uint64_t)xi.idx ^ ((uint64_t)xi.cur[0] << 20), (uint64_t)xi.cur[1] ^
+                                                     (uint64_t)xi.cur[2] ^ (uint64_t)xi.sb[0], lane) : 0;
+            x = wave_sum_i64(x);
+            dbg_x1 = (uint64_t)x;
+        }
+#endif
         // P2: export(b - 1).  A node export(b - 2) holds too keeps that slot (its state and key superseded: x2s = -1);
         // the others take slots [n2, nin)
         if (wave == 0) {
@@ -923,6 +948,14 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                                       m.ti, nT, &ro)) {
                         ++nresc;
                         if (lane == 0) ++L->stats[4];
+#if KSCHED_XCHG_DEBUG
+                        if (A.xp && A.xp->xdbg && lane == 0 && nresc <= 4 && A.dbg_act >= 0 && A.dbg_act < A.xp->xdbg_cap) {
+                            uint64_t *d = A.xp->xdbg + xdbg_commit_off(A.xp->xdbg_cap, A.xp->B, A.xp->R, K) +
+                                          (size_t)A.xp->xdbg_cap * 8 + (size_t)A.dbg_act * 8 + 2 * (nresc - 1);
+                            d[0] = (uint64_t)(uint32_t)f | (uint64_t)(uint32_t)ro.idx << 32;  // diagnostics: the rescue
+                            d[1] = (uint64_t)__double_as_longlong(ro.key);
+                        }
+#endif
                         const bool ht = wi != kNoIdx;
                         if (ro.idx != kNoIdx && !(ht && better(wk, wi, ro.key, ro.idx))) {
                             kf = 1;  // a first touch of a node no candidate list held
@@ -1048,6 +1081,13 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         }
         base += __popcll(mask);
     }
+#if KSCHED_XCHG_DEBUG
+    if (COH && A.xp && A.xp->xdbg && A.dbg_act >= 0 && A.dbg_act < A.xp->xdbg_cap) {  // diagnostics: the outputs
+        int64_t x = lane < done ? (int64_t)dbg_mix((uint64_t)(uint32_t)my_idx, (uint64_t)__double_as_longlong(my_score), lane) : 0;
+        x = wave_sum_i64(x);
+        if (lane == 0) A.xp->xdbg[xdbg_commit_off(A.xp->xdbg_cap, A.xp->B, A.xp->R, K) + (size_t)A.dbg_act * 8 + 3] = (uint64_t)x;
+    }
+#endif
     if (lane == 0) {
         if (COH) {
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
@@ -1064,6 +1104,16 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             add_i64<COH>(&A.ctl->stats[2], placed);
             plan_after_commit<COH>(A, done < nb, p0 + done);
         }
+#if KSCHED_XCHG_DEBUG
+        if (COH && A.xp && A.xp->xdbg && A.dbg_act >= 0 && A.dbg_act < A.xp->xdbg_cap) {  // diagnostics
+            uint64_t *d = A.xp->xdbg + xdbg_commit_off(A.xp->xdbg_cap, A.xp->B, A.xp->R, K) + (size_t)A.dbg_act * 8;
+            d[0] = (uint64_t)p0;
+            d[1] = (uint64_t)done | (uint64_t)nresc << 16 | (uint64_t)nrounds << 32 | (uint64_t)nfail << 48;
+            d[2] = (uint64_t)n1 | (uint64_t)n2 << 16 | (uint64_t)nin << 32 | (uint64_t)base << 48;
+            d[4] = dbg_x1;
+            d[7] = (uint64_t)A.batch;
+        }
+#endif
         if (A.trace_row)  // rounds | rescues << 16 | resolved pods << 24 | failed guesses << 32 | pods resolved one by one << 48
             A.trace_row[16] = (uint64_t)nrounds | (uint64_t)nresc << 16 | (uint64_t)done << 24 | (uint64_t)nfail << 32 |
                               (uint64_t)nseq << 48;

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <tuple>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -174,6 +175,8 @@ struct ksched_ctx {
     int prog_G = 0, prog_B = 0, prog_rows = 0;
     uint64_t *d_trace = nullptr;  // KSCHED_PERSIST_TRACE: per-batch wall-clock stamps
     int64_t trace_cap = 0;
+    uint64_t *d_xdbg = nullptr;      // KSCHED_XCHG_DUMP: the exchange's message hashes (PersistArgs::xdbg)
+    int64_t xdbg_cap = 0, xdbg_calls = 0;
     uint64_t *d_trace_wg = nullptr;  // KSCHED_TRACE_WG: per batch and score workgroup {start, arrival}
     int64_t trace_wg_elems = 0;
     size_t pws_bytes = 0;
@@ -200,6 +203,7 @@ struct ksched_ctx {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
         bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
+        int xchg_diag = 0;       // KSCHED_XCHG_DIAG (section 6.1's experiment): 1 ring zeroed by hipMemsetAsync, 2 local tags from 1
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
         int rescue_max = 4;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
@@ -344,21 +348,65 @@ void fill_xchg_args(const ksched_ctx *c, PersistArgs *a) {
 // granule of an earlier setup, and every setup's epochs start at 1 (tag 0 is never live) -- the one epoch rule
 // of both paths.  Uncached (hipDeviceMallocUncached): a peer GPU's xGMI stores and this GPU's polls meet in
 // memory, never in a stale L2 line.
-int rx_prepare(ksched_ctx *c, size_t bytes, bool uncached) {
-    if (c->d_rx && (c->rx_bytes < bytes || c->rx_uncached != uncached)) {
-        hipFree(c->d_rx);
-        c->d_rx = nullptr;
-        c->rx_bytes = 0;
+// Uncached rings are never given back to the allocator: a page the allocator hands out uncached and later cached
+// again (or the reverse) was read stale by the cached side -- L2 lines of its earlier cached use survive the uncached
+// stores, and a later buffer on those pages (a group's node rows) read them back: the round-4 exchange failure
+// (DESIGN.md section 6.1).  A process-wide pool per device keeps every uncached page uncached for good.
+struct UcPool {
+    std::mutex mu;
+    std::vector<std::tuple<int, void *, size_t>> free;  // (device, block, bytes)
+};
+UcPool &uc_pool() {
+    static UcPool *p = new UcPool();  // never destroyed: its blocks outlive every context
+    return *p;
+}
+hipError_t uc_alloc(int dev, size_t bytes, void **out, size_t *got) {
+    UcPool &P = uc_pool();
+    {
+        std::lock_guard<std::mutex> lk(P.mu);
+        size_t best = SIZE_MAX;
+        int bi = -1;
+        for (int i = 0; i < (int)P.free.size(); ++i) {
+            const auto &[d, q, n] = P.free[(size_t)i];
+            if (d == dev && n >= bytes && n < best) { best = n; bi = i; }
+        }
+        if (bi >= 0) {
+            *out = std::get<1>(P.free[(size_t)bi]);
+            *got = best;
+            P.free.erase(P.free.begin() + bi);
+            return hipSuccess;
+        }
     }
+    *got = bytes;
+    return hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached);
+}
+void uc_release(int dev, void *p, size_t bytes) {
+    UcPool &P = uc_pool();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.free.emplace_back(dev, p, bytes);
+}
+void rx_free(ksched_ctx *c) {
+    if (c->d_rx) {
+        if (c->rx_uncached) uc_release(c->dev, c->d_rx, c->rx_bytes);
+        else hipFree(c->d_rx);
+    }
+    c->d_rx = nullptr;
+    c->rx_bytes = 0;
+}
+
+int rx_prepare(ksched_ctx *c, size_t bytes, bool uncached) {
+    if (c->d_rx && (c->rx_bytes < bytes || c->rx_uncached != uncached)) rx_free(c);
     if (!c->d_rx) {
-        if (uncached) HIPCHK(c, hipExtMallocWithFlags(&c->d_rx, bytes, hipDeviceMallocUncached));
+        size_t got = bytes;
+        if (uncached) HIPCHK(c, uc_alloc(c->dev, bytes, &c->d_rx, &got));
         else HIPCHK(c, hipMalloc(&c->d_rx, bytes));
-        c->rx_bytes = bytes;
+        c->rx_bytes = got;
         c->rx_uncached = uncached;
     }
     // zeroed by system-scope stores, the granules' own path (a hipMemsetAsync of an uncached ring was not what the
     // persistent kernel's system-scope loads read afterwards: the round-4 failure)
-    HIPCHK(c, launch_zero_sys(c->d_rx, c->rx_bytes, c->stream));
+    if (c->diag.xchg_diag & 1) HIPCHK(c, hipMemsetAsync(c->d_rx, 0, c->rx_bytes, c->stream));  // round 4's way
+    else HIPCHK(c, launch_zero_sys(c->d_rx, c->rx_bytes, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return KSCHED_OK;
 }
@@ -420,7 +468,7 @@ int decide_fast53(ksched_ctx *c) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (mn < 0) {
             c->xchg_ready = false;
-            hipMemset(c->d_err, 0, sizeof(int32_t));
+            (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
             return fail(c, KSCHED_E_DEVICE, "node-sharded exchange: a peer rank never met this one (device barrier timed out)");
         }
         flag = mn;
@@ -847,6 +895,20 @@ int enqueue_persistent(ksched_ctx *c) {
         a.trace_wg = c->d_trace_wg;
         a.trace_cap = c->trace_wg_elems / G;
     }
+    if (const char *xd = std::getenv("KSCHED_XCHG_DUMP"); xd && *xd && c->xchg_run) {
+        const int64_t cap = 4 * (c->p / B) + 64;
+        const int64_t elems = (int64_t)xdbg_commit_off(cap, B, c->o.nranks, c->K) + cap * 16;
+        if (c->xdbg_cap < cap) {
+            if (c->d_xdbg) hipFree(c->d_xdbg);
+            c->d_xdbg = nullptr;
+            c->xdbg_cap = 0;
+            HIPCHK(c, hipMalloc(&c->d_xdbg, (size_t)elems * 8));
+            c->xdbg_cap = cap;
+        }
+        HIPCHK(c, hipMemsetAsync(c->d_xdbg, 0, (size_t)elems * 8, c->stream));
+        a.xdbg = c->d_xdbg;
+        a.xdbg_cap = cap;
+    }
     if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
     if (c->d_dbg) {
         HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), c->stream));
@@ -1013,6 +1075,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
     c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
+    c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
@@ -1042,7 +1105,8 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
         ksched_destroy(c);
         return KSCHED_E_DEVICE;
     }
-    if (hipMemset(c->d_err, 0, sizeof(int32_t)) != hipSuccess) {  // error word read by every sync
+    if (hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream) != hipSuccess ||  // error word read by every sync
+        hipStreamSynchronize(c->stream) != hipSuccess) {
         ksched_destroy(c);
         return KSCHED_E_DEVICE;
     }
@@ -1071,10 +1135,10 @@ int ksched_destroy(ksched_ctx *c) {
     }
     for (int i = 0; i < 3; ++i) if (c->ev_pipe[i]) hipEventDestroy(c->ev_pipe[i]);
     hipFree(c->d_xring); hipFree(c->d_lring);
-    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_trace_wg); hipFree(c->d_xmin);
+    hipFree(c->d_xws); hipFree(c->d_xbuf); hipFree(c->d_pws); hipFree(c->d_trace); hipFree(c->d_trace_wg); hipFree(c->d_xdbg); hipFree(c->d_xmin);
     rx_unmap_peers(c);
     c->lg.reset();
-    hipFree(c->d_rx);
+    rx_free(c);
     if (c->stream) hipStreamDestroy(c->stream);
     if (c->stream2) hipStreamDestroy(c->stream2);
     delete c;
@@ -1254,7 +1318,7 @@ int ksched_xchg_join_local_ex(ksched_ctx *const *ctxs, int32_t n, int32_t flags)
         }
     }
     // the same epoch rule as xchg_import: the process's first unused tag (one process: one hint)
-    const uint32_t e0 = std::max<uint32_t>(1u, g_epoch_next.load());
+    const uint32_t e0 = (c0->diag.xchg_diag & 2) ? 1u : std::max<uint32_t>(1u, g_epoch_next.load());  // 2: round 4's tags
     epoch_used_below(e0 + 1);
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
@@ -1301,7 +1365,10 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, grow(&c->d_nodes, &c->node_cap, n, sizeof(NodeRec)));
     if (c->d_snap) { hipFree(c->d_snap); c->d_snap = nullptr; }
-    if (n > 0) HIPCHK(c, hipMemcpy(c->d_nodes, h.data(), (size_t)n * sizeof(NodeRec), hipMemcpyHostToDevice));
+    // in the stream of the kernels that read it (a legacy hipMemcpy from pageable memory may return before its DMA
+    // lands, and nothing orders it with this non-blocking stream: k_prep_nodes read the memory's earlier contents --
+    // the round-4 exchange failure)
+    if (n > 0) HIPCHK(c, hipMemcpyAsync(c->d_nodes, h.data(), (size_t)n * sizeof(NodeRec), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, launch_prep_nodes(c->d_nodes, n, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->max_abs_alloc = mx;
@@ -1333,8 +1400,8 @@ int ksched_apply_delta(ksched_ctx *c, int64_t k, const int32_t *idx, const int64
     int64_t *d_d = nullptr;
     HIPCHK(c, hipMalloc(&d_idx, (size_t)k * 4));
     if (hipMalloc(&d_d, (size_t)k * 24) != hipSuccess) { hipFree(d_idx); return fail(c, KSCHED_E_DEVICE, "apply_delta: alloc"); }
-    hipError_t e = hipMemcpy(d_idx, idx, (size_t)k * 4, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d_d, d.data(), (size_t)k * 24, hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(d_idx, idx, (size_t)k * 4, hipMemcpyHostToDevice, c->stream);  // the kernel's stream
+    if (e == hipSuccess) e = hipMemcpyAsync(d_d, d.data(), (size_t)k * 24, hipMemcpyHostToDevice, c->stream);
     c->explain_valid = false;
     if (e == hipSuccess) e = launch_apply_delta(c->d_nodes, c->n_local, k, d_idx, d_d, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1513,11 +1580,14 @@ int ksched_upload_pods(ksched_ctx *c, int64_t p, const int64_t *rc, const int64_
         c->p_cap = p;
     }
     if (p > 0) {
-        HIPCHK(c, hipMemcpy(c->d_rc, rc, (size_t)p * 8, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->d_rm, rm, (size_t)p * 8, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->d_rp, rp, (size_t)p * 8, hipMemcpyHostToDevice));
-        if (sel) HIPCHK(c, hipMemcpy(c->d_sel, sel, (size_t)p * 8, hipMemcpyHostToDevice));
-        else HIPCHK(c, hipMemset(c->d_sel, 0, (size_t)p * 8));
+        // in the stream of the kernels that read them, finished before the caller's buffers may change (see
+        // ksched_load_nodes)
+        HIPCHK(c, hipMemcpyAsync(c->d_rc, rc, (size_t)p * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_rm, rm, (size_t)p * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_rp, rp, (size_t)p * 8, hipMemcpyHostToDevice, c->stream));
+        if (sel) HIPCHK(c, hipMemcpyAsync(c->d_sel, sel, (size_t)p * 8, hipMemcpyHostToDevice, c->stream));
+        else HIPCHK(c, hipMemsetAsync(c->d_sel, 0, (size_t)p * 8, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
     }
     uint64_t sum = 0;
     for (int64_t i = 0; i < p; ++i) sum = sat_add(sum, sat_add(uabs(rc[i]), sat_add(uabs(rm[i]), uabs(rp[i]) + 1)));
@@ -1534,8 +1604,8 @@ int ksched_selftest_fastdiv(ksched_ctx *c, int64_t n, const double *a, const dou
     HIPCHK(c, hipSetDevice(c->dev));
     double *d = nullptr;
     HIPCHK(c, hipMalloc(&d, (size_t)n * 32));
-    hipError_t e = hipMemcpy(d, a, (size_t)n * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(d + n, b, (size_t)n * 8, hipMemcpyHostToDevice);
+    hipError_t e = hipMemcpyAsync(d, a, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + n, b, (size_t)n * 8, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_selftest_div(n, d, d + n, d + 2 * n, d + 3 * n, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(out_native, d + 2 * n, (size_t)n * 8, hipMemcpyDeviceToHost);
@@ -1714,6 +1784,21 @@ static int sync_impl(ksched_ctx *c) {
         print_persist_trace(c);
         print_wg_busy(c);
     }
+    // KSCHED_XCHG_DUMP=<path>: the exchange's message hashes, to <path>.r<rank>.c<call> ([cap][B][R + 1] u64)
+    if (c->persist_stats && c->d_xdbg && c->xchg_run) {
+        if (const char *xd = std::getenv("KSCHED_XCHG_DUMP"); xd && *xd) {
+            const size_t elems = xdbg_commit_off(c->xdbg_cap, c->B, c->o.nranks, c->K) + (size_t)c->xdbg_cap * 16;
+            std::vector<uint64_t> t(elems);
+            if (hipMemcpy(t.data(), c->d_xdbg, elems * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                const std::string path = std::string(xd) + ".r" + std::to_string(c->o.rank) + ".c" + std::to_string(c->xdbg_calls);
+                if (FILE *f = std::fopen(path.c_str(), "wb")) {
+                    std::fwrite(t.data(), 8, t.size(), f);
+                    std::fclose(f);
+                }
+            }
+        }
+        ++c->xdbg_calls;
+    }
     // KSCHED_TRACE_WG=<path>: the raw per-workgroup stamps ([batches][G] u64: scan start | arrival << 32)
     if (c->persist_stats && c->d_trace_wg && c->prog_G > 0) {
         if (const char *wgp = std::getenv("KSCHED_TRACE_WG"); wgp && *wgp) {
@@ -1757,7 +1842,7 @@ static int sync_impl(ksched_ctx *c) {
         c->xchg_run = false;
     }
     if (e >= 5 && e <= 11) {
-        hipMemset(c->d_err, 0, sizeof(int32_t));
+        (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
         static const std::string lagw = "a score or merger workgroup's wait for commit(b-" + std::to_string(kPipeLag) + ")";
         static const char *what[] = {"the commit's wait for the merges", lagw.c_str(),
                                      "a merger's wait for the score workgroups", "the score grid's plan (idle)",
@@ -1775,7 +1860,7 @@ static int sync_impl(ksched_ctx *c) {
         return fail(c, KSCHED_E_DEVICE, std::string(buf) + progress_summary(c));
     }
     if (e == 2 || e == 4) {
-        hipMemset(c->d_err, 0, sizeof(int32_t));
+        (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
         return fail(c, KSCHED_E_DEVICE, e == 2 ? "batched mode: the merge's wait for the score workgroups timed out"
                                                : "batched mode: the score's wait for commit(b-2) timed out");
     }

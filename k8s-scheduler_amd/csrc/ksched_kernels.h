@@ -283,7 +283,20 @@ struct CommitArgs {
     int32_t *err;           // device error word (12 = the rescue wait timed out)
     uint64_t *trace_row;    // KSCHED_PERSIST_TRACE: this batch's trace row (else null)
     const PersistArgs *xp;  // persistent pipeline: its arguments (R > 1: the rescue's rank fold through the rings)
+    int64_t dbg_act;        // diagnostics (KSCHED_XCHG_DUMP): this batch's active-batch index
 };
+// KSCHED_XCHG_DUMP's list sums: (key, idx | valid) words of a pod's merged list as written / as the commit loaded
+// them, [cap][B][2] u64 after the hashes and the messages
+__device__ __forceinline__ uint64_t dbg_mix(uint64_t w0, uint64_t w1, int q) {
+    return (w0 * 0x9e3779b97f4a7c15ull + w1) * (uint64_t)(2 * q + 1);
+}
+__host__ __device__ inline size_t xdbg_sums_off(int64_t cap, int B, int R, int K) {
+    return (size_t)cap * B * (R + 1) + ((size_t)16 * B * (K * 14 + 2) + 1) / 2;
+}
+// ... then per active batch the commit's summary [cap][8] u64 (ksched_commit.h)
+__host__ __device__ inline size_t xdbg_commit_off(int64_t cap, int B, int R, int K) {
+    return xdbg_sums_off(cap, B, R, K) + (size_t)cap * B * 2;
+}
 
 // Commit(b) -> score(b + lag) hand-off on the device (lag 2 on the stream pipeline, kPipeLag in k_pipe): the
 // committing wave drains its stores, writes back the XCD L2 (agent release) and publishes
@@ -438,11 +451,15 @@ struct PersistArgs {
     // optional (KSCHED_TRACE_WG=<path>): per batch and score workgroup {scan start, arrival} as the low and
     // high 32 bits of the 100 MHz wall clock, [trace_cap][G]
     uint64_t *trace_wg;
+    // optional (KSCHED_XCHG_DUMP=<path>, R > 1): per active batch a and pod m, [R + 1] hashes of the messages the
+    // merger received from each rank, then of the one it sent: [(a * B + m) * (R + 1) + r]
+    uint64_t *xdbg;
+    int64_t xdbg_cap;       // active batches it holds
     int64_t *cdbg;  // KSCHED_COMMIT_STAMPS: commit phase cycle sums (CommitArgs::dbg), else null
     int64_t *mdbg;  // KSCHED_MERGE_STAMPS: merge phase cycle sums (MergeArgs::dbg), else null
     // node-sharded (R > 1, one process per GPU): this rank owns global nodes [node_offset, +n_local);
     // merger m of every rank writes pod m's list into EVERY rank's receive ring (rx_peer[r], slot
-    // (active batch % 4, source rank, pod) of xchg_stride bytes) as tagged 8-byte granules {word, tag},
+    // (active batch % 4, source rank, pod) of xchg_stride bytes) as tagged 8-byte granules (gran_enc),
     // then gathers the R lists of pod m from its own ring and rank-merges them (ksched_persist.hip)
     int64_t node_offset;
     int32_t R, rank;
@@ -523,6 +540,21 @@ __device__ __forceinline__ bool poll_ge(const unsigned long long *p, unsigned lo
         }
     }
 }
+// The exchange's 8-byte granules carry one 32-bit word and the writer's tag in EACH 32-bit half: {tag16 | word
+// bits 0..15} low, {tag16 | word bits 16..31} high, tag16 = (tag & 0x7fff) | 0x8000 (never 0: a zeroed ring holds no
+// live granule).  A reader accepts the granule only when both halves carry the tag, so a granule read half old and
+// half new (an 8-byte access split into two 4-byte ones -- seen on uncached rings) is never
+// taken for the new one.  Tags 32768 apart would alias; a ring region is rewritten every 4 active batches.
+__device__ __forceinline__ uint32_t gran_tag(uint32_t tag) { return (tag & 0x7fffu) | 0x8000u; }
+__device__ __forceinline__ uint64_t gran_enc(uint32_t word, uint32_t t16) {
+    return ((uint64_t)((t16 << 16) | (word >> 16)) << 32) | (uint64_t)((t16 << 16) | (word & 0xffffu));
+}
+__device__ __forceinline__ bool gran_dec(uint64_t v, uint32_t t16, uint32_t *word) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    *word = (lo & 0xffffu) | (hi << 16);
+    return ((lo >> 16) == t16) & ((hi >> 16) == t16);
+}
+
 constexpr int kMaxXchgRanks = 8;
 // receive ring: [4 active-batch slots][R source ranks][B pods] messages, then R barrier granules, then the
 // rescue area: [2 request parities][R source ranks] one Rec as 14 tagged granules (128 bytes each)

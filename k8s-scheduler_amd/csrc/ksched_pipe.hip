@@ -44,6 +44,9 @@ constexpr int kMT = kPipeMergeThreads; // threads of one pod merge: one per scor
 constexpr int kMW = kMT / 64;          // waves of one pod merge
 constexpr int kMS = kPipeMergeSlots;   // pod merges per merger workgroup
 constexpr int kPU = 4;                 // rows per score step (independent key chains)
+#ifndef KSCHED_XCHG_DEBUG
+#define KSCHED_XCHG_DEBUG 0
+#endif
 #ifndef KSCHED_SCREEN_PU
 #define KSCHED_SCREEN_PU 4
 #endif
@@ -82,26 +85,24 @@ __device__ __forceinline__ bool spin_ge(const PersistArgs &P, int slot, const un
 // the first failure names the wait that timed out (ksched_sync reports it)
 __device__ __forceinline__ void set_err(int32_t *err, int32_t code) { atomicCAS(err, 0, code); }
 
-// Cross-device granules: system-scope relaxed 8-byte accesses (global_store/load ... sc0 sc1) on the
-// uncached receive rings; an 8-byte store arrives whole, so a granule whose tag matches holds its word.
+// Cross-device granules: system-scope relaxed 8-byte accesses (global_store/load ... sc0 sc1) on the receive
+// rings, the tag in both 32-bit halves (gran_enc): a granule is taken only when both halves are the writer's.
 __device__ __forceinline__ void st_sys(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint64_t ld_sys(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// poll one granule until it carries `tag` (false: timed out)
+// poll one granule until both its halves carry `tag` (gran_dec; false: timed out)
 __device__ __forceinline__ bool granule_wait(const uint64_t *p, uint32_t tag, int64_t limit, uint32_t *word) {
-    uint64_t v = ld_sys(p);
-    if ((uint32_t)(v >> 32) != tag) {
+    const uint32_t t16 = gran_tag(tag);
+    if (!gran_dec(ld_sys(p), t16, word)) {
         const uint64_t t0 = wall_clock64();
         do {
             if ((int64_t)(wall_clock64() - t0) > limit) return false;
             __builtin_amdgcn_s_sleep(1);
-            v = ld_sys(p);
-        } while ((uint32_t)(v >> 32) != tag);
+        } while (!gran_dec(ld_sys(p), t16, word));
     }
-    *word = (uint32_t)v;
     return true;
 }
 
@@ -1149,7 +1150,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
                     const int r = e / MW, w = e % MW;
                     uint64_t *dst = reinterpret_cast<uint64_t *>(
                         P.rx_peer[r] + ((size_t)(slot * RR + P.rank) * P.B + m) * (size_t)P.xchg_stride);
-                    st_sys(dst + w, (uint64_t)s_msg[w] | ((uint64_t)tag << 32));
+                    st_sys(dst + w, gran_enc(s_msg[w], gran_tag(tag)));
                 }
                 bool ok = true;
                 const char *own = P.rx_peer[P.rank];
@@ -1164,10 +1165,32 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
                 if (!ok) { set_err(P.err, 10); pc->m_stop = 1; }
                 sync();
                 if (pc->m_stop) return;
+#if KSCHED_XCHG_DEBUG  // diagnostics build (tools/xchg_ring_experiment.py): message hashes and the first messages
+                if (P.xdbg && mtid <= RR && nact - 1 < P.xdbg_cap) {  // diagnostics: the messages as received / sent
+                    const uint32_t *msg = mtid < RR ? s_all + mtid * MW : s_msg;
+                    uint64_t h = 0x9e3779b97f4a7c15ull;
+                    for (int w = 0; w < MW; ++w) h = (h ^ msg[w]) * 0x100000001b3ull;
+                    P.xdbg[((size_t)(nact - 1) * P.B + m) * (RR + 1) + mtid] = h;
+                }
+                if (P.xdbg && nact - 1 < 16) {  // diagnostics: the first 16 active batches' sent messages, whole
+                    uint32_t *xm = reinterpret_cast<uint32_t *>(P.xdbg + (size_t)P.xdbg_cap * P.B * (RR + 1)) +
+                                   ((size_t)(nact - 1) * P.B + m) * MW;
+                    for (int w = mtid; w < MW; w += kMT) xm[w] = s_msg[w];
+                }
+#endif
                 if (mtid < 64) rank_merge_msgs<K>(s_all, RR, ma.out_rec + (size_t)m * K, ma.out_fc + m);
             }
             drain_stores();
             sync();  // every merge wave's stores drained before the count; LDS free for the next pod
+#if KSCHED_XCHG_DEBUG
+            if (P.xdbg && mtid < 64 && nact - 1 < P.xdbg_cap && p0 + m < NP) {  // diagnostics: the list as written
+                const uint64_t *w = reinterpret_cast<const uint64_t *>(ma.out_rec + (size_t)m * K + (mtid < K ? mtid : 0));
+                int64_t x = mtid < K ? (int64_t)dbg_mix(ld_coh(w), ld_coh(w + 1), mtid) : 0;
+                x = wave_sum_i64(x);
+                if (mtid == 0)
+                    P.xdbg[xdbg_sums_off(P.xdbg_cap, P.B, P.R, K) + ((size_t)(nact - 1) * P.B + m) * 2] = (uint64_t)x;
+            }
+#endif
             if (mtid == 0) {
                 if (m == 0) st_coh(&ctl->nact, (uint64_t)nact);
                 const unsigned long long d =
@@ -1214,13 +1237,15 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
     int64_t nact = 0;  // active batches among 0 .. b (both workgroups' batches)
     int idle = 0;
     for (int64_t b = par;; b += 2) {
-        // the plans of b - 1 and b were set by commits b - 4 and b - 3 (or k_ctl_init), both published before
-        // this workgroup's commit(b - 2) finished
-        const int64_t p0 = (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
-        const int64_t pm = b >= 1 ? (int64_t)ld_coh(&ctl->plan[(b - 1) % kPlanRing]) : -1;
+        // the plans of b - 1 and b were set by commits b - 4 and b - 3 (or k_ctl_init).  Both are in this
+        // workgroup's LDS copy already: plan(b - 1) from its own commit(b - 4) (persist_plan), plan(b) from the
+        // hand-off record commit(b - 2) received (commit(b - 3) drains nothing in front of the record, so its
+        // store to Ctl::plan may still be in flight here).  Only the plans k_ctl_init set come from memory.
+        const int64_t p0 = b >= 2 ? loc.plan[b % kPlanRing] : (int64_t)ld_coh(&ctl->plan[b % kPlanRing]);
+        const int64_t pm = b >= 4 ? loc.plan[(b - 1) % kPlanRing] : b >= 1 ? (int64_t)ld_coh(&ctl->plan[(b - 1) % kPlanRing]) : -1;
         const bool act = p0 >= 0 && p0 < P.pods.p;
         nact += ((b >= 1 && pm >= 0 && pm < P.pods.p) ? 1 : 0) + (act ? 1 : 0);
-        if (threadIdx.x == 0) loc.plan[b % kPlanRing] = p0;
+        if (b < 2 && threadIdx.x == 0) loc.plan[b % kPlanRing] = p0;
         if (!act && ++idle > kPlanRing) {
             // pods remain but nothing is planned: a truncation re-plans within kPipeLag batches, so this is a
             // protocol error -- stop everyone instead of spinning
@@ -1341,6 +1366,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         ca.loc = &loc;
         ca.rescue = P.rescue;  // null: an exhausted list truncates its batch (KSCHED_RESCUE_MAX=0)
         ca.xp = &P;            // R > 1: the rescue's rank fold
+        ca.dbg_act = nact - 1;
         ca.rescue_n = P.B;
         ca.rescue_max = P.rescue_max;
         ca.inh = P.inh;
@@ -1489,7 +1515,7 @@ __global__ __launch_bounds__(64) void k_xchg_min(PersistArgs P, int32_t mine, in
     const int lane = threadIdx.x;
     const size_t off = (size_t)4 * P.R * P.B * (size_t)P.xchg_stride;
     const uint32_t tag = P.epoch0;
-    if (lane < P.R) st_sys(reinterpret_cast<uint64_t *>(P.rx_peer[lane] + off) + P.rank, (uint64_t)(uint32_t)mine | ((uint64_t)tag << 32));
+    if (lane < P.R) st_sys(reinterpret_cast<uint64_t *>(P.rx_peer[lane] + off) + P.rank, gran_enc((uint32_t)mine, gran_tag(tag)));
     int32_t v = 0x7fffffff;
     bool ok = true;
     if (lane < P.R) {

@@ -65,6 +65,9 @@ case "$1" in
     abl base1 base && abl main1 main && abl base2 base && abl main2 main &&
     trace trace_c4
     ;;
+  xchg_exp)  # DESIGN 6.1's ring experiment
+    soft xchg_exp 900 python -u tools/xchg_ring_experiment.py $XCHG_VARIANTS
+    ;;
   all)
     step pytest_all 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/
     ;;
