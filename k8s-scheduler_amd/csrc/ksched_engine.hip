@@ -223,8 +223,10 @@ int fail(ksched_ctx *c, int code, const std::string &msg) {
 #define HIPCHK(c, expr)                                                                        \
     do {                                                                                       \
         hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess)                                                                  \
+        if (e_ != hipSuccess) {                                                                \
+            (void)hipGetLastError(); /* reported here: not again by a later launch's check */   \
             return fail((c), KSCHED_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+        }                                                                                      \
     } while (0)
 
 #define NCCLCHK(c, expr)                                                                       \
