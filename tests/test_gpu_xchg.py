@@ -177,5 +177,7 @@ def test_xchg_sharded_rescue(gpu_available, oracle_mod, world):
     trunc = {x[5] for x in st}
     assert len(resc) == 1 and len(trunc) == 1, f"ranks disagree on rescues {resc} / truncations {trunc}"
     nres, ntr = resc.pop(), trunc.pop()
+    print(f"sharded rescue R={world}: {nres} rescues, {ntr} truncated batches; one rank: {one['rescues']} rescues, "
+          f"{one['truncations']} truncated")
     assert nres > 0, f"no rescue in {world} ranks (one rank: {one['rescues']} rescues, {one['truncations']} truncated)"
     assert ntr <= 2 * one["truncations"] + 2, f"{world} ranks truncated {ntr} batches, one rank {one['truncations']}"
