@@ -44,6 +44,21 @@ static_assert(spc_slots<true>() + 1 <= kRescueMaxT, "RescueReq::ti must hold the
 constexpr int kSpcInvalid = kSpcHash - 1;  // table position reserved for "no entry" (always taken)
 constexpr int kGS = 14;                     // words per guessed entry in SpcSmem::GS
 
+// The touched-node screen (persistent commit, resource priority).  A pod's key for a touched
+// node matters only where it can beat an untouched entry of the pod's list -- each of which keys at or above the
+// list's last entry -- or where no untouched entry is left: a complete (not cut) list then takes the best touched
+// node, a cut one compares it with its last entry (below it: rescue or truncation).  So a pair whose f32 screen
+// (screen_pair: |screen - key| < 1.3e-5, or NaN) lies below thr = RN_f32(last key - 5e-5) of a CUT list keys
+// below every entry of the list, and its exact key is skipped: S holds kSkipKey (a NaN, which no comparison ranks)
+// instead.  Only the rescue of an exhausted cut list compares touched nodes below the last entry; it re-keys the
+// pod's skipped slots first (rekey_row).  On c4 about 0.1 % of these pairs could matter.
+constexpr uint64_t kSkipKeyBits = 0x7ff8000000000badull;
+__device__ __forceinline__ double skip_key() { return __longlong_as_double((long long)kSkipKeyBits); }
+// the f32 reciprocal the screen takes, from the refined f64 one (screen_recip's domain: NaN unless 0 < a < 2^52)
+__device__ __forceinline__ float screen_y(int64_t a, double y) {
+    return (a > 0 && a < (1ll << 52)) ? (float)y : __builtin_nanf("");
+}
+
 struct alignas(8) SpcSlot {
     int32_t idx;
     int32_t mine;     // committed by this batch (exported)
@@ -79,6 +94,7 @@ struct SpcSmem {
                       // step 1 only (aliases pbk/pbx, which steps 2-3 use)
     uint64_t *GS;     // [64 pods][kGS] each pod's guessed entry: state a[3], labels, price, and the state after
                       // the pod's commit n[3] with its (double) and refined reciprocals (computed once, lane = pod)
+    float *thr;       // [64] per pod: a touched node's key screens below this -> it cannot matter (kSkipKey)
     // persistent commit: the slots of the older export (batch b - 2) are keyed by the merger workgroups
     int16_t *x2s;     // [64] slot of that export's entry e (-1: the node is also in export(b - 1): no slot)
 };
@@ -333,6 +349,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     constexpr int kSpcWaves = NT / 64;
     constexpr int kSpcThreads = NT;
     constexpr bool LAG3 = COH;  // the persistent pipeline runs at lag kPipeLag = 3
+    constexpr bool SCR = COH && PRIO != kPrioPrice;  // the touched-node screen (above)
     static_assert(!COH || kPipeLag == 3, "commit_spc_batch: the persistent pipeline's inheritance is lag 3");
     constexpr int kSpcRow = spc_slots<LAG3>() + 1;
     const int tid = threadIdx.x;
@@ -403,6 +420,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
         m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
+        m.thr = reinterpret_cast<float *>(p); p += 64 * sizeof(float);
         m.x2s = reinterpret_cast<int16_t *>(p); p += 64 * sizeof(int16_t);
         m.D = reinterpret_cast<int8_t *>(p);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
@@ -456,6 +474,9 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         int dfl = 0;
         double pk = -__builtin_inf();
         int32_t pi = kNoIdx, ps = -1;
+        const float thrf = SCR ? m.thr[lane] : 0.0f;
+        const float qc = screen_req(rc), qm = screen_req(rm), qp = screen_req(rp);
+        int64_t nex = 0;
         for (int e = wave; e < ne; e += kSpcWaves) {
             const int t = sl(e);
             const SpcSlot &x = m.T[t];
@@ -464,10 +485,22 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             const bool f1 = fits(rc, rm, rp, sel, x.cur[0], x.cur[1], x.cur[2], x.labels, LAB);
             dfl += (int)f1 - (int)f0;
             const double *yy = m.iy + e * 6;  // the entry's state as doubles and its reciprocals, staged once
+            bool need = true;
+            if constexpr (SCR) {
+                bool lo;
+                const float v = screen_pair(qc, qm, qp, screen_y(x.cur[0], yy[3]), screen_y(x.cur[1], yy[4]),
+                                            screen_y(x.cur[2], yy[5]), x.cur[0] >= rc, x.cur[1] >= rm, x.cur[2] >= rp, &lo);
+                need = pj && !(v < thrf);
+            }
             double k;
-            const bool el = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
-                                                          yy[0], yy[1], yy[2], yy[3], yy[4], yy[5], y3, x.price, &k);
-            k = el ? k : -__builtin_inf();
+            if (!SCR || __ballot(need) != 0) {
+                ++nex;
+                const bool el = pair_key_fast<PRIO, DOM, F53>(f1, rc, rm, rp, rcf, rmf, rpf, x.cur[0], x.cur[1], x.cur[2],
+                                                              yy[0], yy[1], yy[2], yy[3], yy[4], yy[5], y3, x.price, &k);
+                k = el ? k : -__builtin_inf();
+            } else {
+                k = skip_key();
+            }
             Srow[t] = k;
             const bool up = k != -__builtin_inf() && better(k, x.idx, pk, pi);
             pk = up ? k : pk; pi = up ? x.idx : pi; ps = up ? t : ps;
@@ -475,6 +508,10 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         m.pbk[wave * 64 + lane] = pk;
         m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
         if (dfl != 0) atomicAdd(&m.dfacc[lane], dfl);
+        if (SCR && A.dbg && lane == 0 && wave < ne) {  // diagnostics: entries keyed, exactly
+            atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[16]), (unsigned long long)((ne - 1 - wave) / kSpcWaves + 1));
+            atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[17]), (unsigned long long)nex);
+        }
     };
     // the batch's candidate lists -> LK / LI and their table positions HP
     auto hash_lists = [&]() {
@@ -588,6 +625,20 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             const int i = tid + u * kSpcThreads;
             if (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) m.S[(size_t)(i >> 6) * kSpcRow + (i & 63)] = x2v[u];
         }
+        if constexpr (SCR) {  // the touched-node screen's thresholds (the hand-off's barrier publishes them)
+            __syncthreads();  // LK / LI complete
+            if (wave == 0) {
+                float t = -__builtin_inff();  // complete lists (and lanes past the batch): never skipped
+                if (pj && cut0) {
+                    int n = 0;  // the list length (valid entries form a prefix): a binary search
+#pragma unroll
+                    for (int st = K; st >= 1; st >>= 1)
+                        if (n + st <= K && m.LI[(n + st - 1) * 64 + lane] != kNoIdx) n += st;
+                    if (n > 0) t = (float)(m.LK[(n - 1) * 64 + lane] - 5e-5);
+                }
+                m.thr[lane] = t;
+            }
+        }
         // ---- the hand-off: commit(b - 1) published (a workgroup barrier) ----
         // (wave 0 lane e < n1 receives entry e of export(b - 1) with the record: the same round of loads)
         HandoffRes ho;
@@ -699,8 +750,36 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         if (lane == 0) { m.ctl[0] = 0; m.ctl[2] = 0; }
     }
 
+    // wave 0: pod f's exact best touched slot, its screened-out slots re-keyed (the rescue compares below the last
+    // list entry); (wk, wi, s) holds the best of the slots it keyed exactly
+    auto rekey_row = [&](int f, double &wk, int32_t &wi, int &s) {
+        const int64_t fc = rl64(rc, f), fm = rl64(rm, f), fp = rl64(rp, f);
+        const uint64_t fs = (uint64_t)rl64((int64_t)sel, f);
+        const double fcf = (double)fc, fmf = (double)fm, fpf = (double)fp;
+        double *row = m.S + (size_t)f * kSpcRow;
+        int64_t nrk = 0;
+        for (int t0 = 0; t0 < nT; t0 += 64) {
+            const int t = t0 + lane;
+            double k = -__builtin_inf();
+            int32_t x = kNoIdx, ts_ = t;
+            if (t < nT && row[t] != row[t]) {  // skipped
+                const SpcSlot &y = m.T[t];
+                const bool fy = fits(fc, fm, fp, fs, y.cur[0], y.cur[1], y.cur[2], y.labels, LAB);
+                k = lane_key<PRIO, DOM, LAB, F53>(fy, fc, fm, fp, fcf, fmf, fpf, y.cur[0], y.cur[1], y.cur[2], y3, y.price);
+                row[t] = k;
+                x = k != -__builtin_inf() ? y.idx : kNoIdx;
+                ++nrk;
+            }
+            wave_argbest_fast(k, x, ts_);
+            if (x != kNoIdx && better(k, x, wk, wi)) { wk = k; wi = x; s = ts_; }
+        }
+        if (A.dbg && lane == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[22]), 1ull);
+        (void)nrk;
+    };
     int c = 0;
     if (COH && tid == 0 && A.trace_row) A.trace_row[25] = wall_clock64();  // the rounds start
+    uint64_t *const tr1 = (COH && tid == 0) ? A.trace_row : nullptr;  // the first round's stamps (cols 49-51)
+    bool first = true;
     const uint64_t t_pro = dbg ? __builtin_amdgcn_s_memtime() - t_start : 0;
     for (;;) {
         // ---- step 1 (wave 0): guesses for pods [c, cend) ----
@@ -764,6 +843,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             if (lane == 0) { m.ctl[0] = c; m.ctl[1] = cend; }
         }
         __syncthreads();
+        if (first && tr1) tr1[49] = wall_clock64();  // the first guess step done
         if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s1 += t - t_mark; t_mark = t; }
         const int rc0 = m.ctl[0], rce = m.ctl[1];
         // ---- step 2 (all waves): evaluate the guessed commits in parallel ----
@@ -791,6 +871,9 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                 o[13] = (uint64_t)__double_as_longlong(recip_or_zero(n2, nf2));
             }
             __syncthreads();
+            const float thrf = SCR ? m.thr[lane] : 0.0f;
+            const float qc = screen_req(rc), qm = screen_req(rm), qp = screen_req(rp);
+            int64_t nev = 0, nex = 0;
             for (int k = rc0 + wave; k < rce; k += kSpcWaves) {
                 const int32_t g = __builtin_amdgcn_readfirstlane(m.gn[k]);
                 if (g < 0) continue;  // wave-uniform
@@ -803,13 +886,27 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                 const bool fo = fits(rc, rm, rp, sel, a0, a1, a2, lab, LAB);
                 const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
                 const int d = (int)fn - (int)fo;
+                const double ny0 = __longlong_as_double((long long)gsk[11]), ny1 = __longlong_as_double((long long)gsk[12]),
+                             ny2 = __longlong_as_double((long long)gsk[13]);
+                bool need = true;
+                if constexpr (SCR) {  // only the pods after the guessing one use its column
+                    bool lo;
+                    const float v = screen_pair(qc, qm, qp, screen_y(n0, ny0), screen_y(n1, ny1), screen_y(n2, ny2),
+                                                n0 >= rc, n1 >= rm, n2 >= rp, &lo);
+                    need = lane > k && pj && !(v < thrf);
+                }
                 double kv;
-                const bool el = pair_key_fast<PRIO, DOM, F53>(
-                    fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, __longlong_as_double((long long)gsk[8]),
-                    __longlong_as_double((long long)gsk[9]), __longlong_as_double((long long)gsk[10]),
-                    __longlong_as_double((long long)gsk[11]), __longlong_as_double((long long)gsk[12]),
-                    __longlong_as_double((long long)gsk[13]), y3, pr, &kv);
-                kv = el ? kv : -__builtin_inf();
+                ++nev;
+                if (!SCR || __ballot(need) != 0) {
+                    ++nex;
+                    const bool el = pair_key_fast<PRIO, DOM, F53>(
+                        fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, __longlong_as_double((long long)gsk[8]),
+                        __longlong_as_double((long long)gsk[9]), __longlong_as_double((long long)gsk[10]), ny0, ny1, ny2,
+                        y3, pr, &kv);
+                    kv = el ? kv : -__builtin_inf();
+                } else {
+                    kv = skip_key();
+                }
                 Srow[s] = kv;
                 m.D[k * 64 + lane] = (int8_t)d;
                 if (lane > k) {
@@ -828,8 +925,13 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             }
             m.pbk[wave * 64 + lane] = pk;
             m.pbx[wave * 64 + lane] = ((int64_t)ps << 32) | (uint32_t)pi;
+            if (SCR && A.dbg && lane == 0 && nev) {  // diagnostics: guessed columns keyed, exactly
+                atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[18]), (unsigned long long)nev);
+                atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[19]), (unsigned long long)nex);
+            }
         }
         __syncthreads();
+        if (first && tr1) tr1[50] = wall_clock64();  // its evaluation done
         if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s2 += t - t_mark; t_mark = t; }
         // ---- step 3 (wave 0): check, confirm the valid prefix, resolve the first failure ----
         if (wave == 0) {
@@ -956,6 +1058,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                             d[1] = (uint64_t)__double_as_longlong(ro.key);
                         }
 #endif
+                        if constexpr (SCR) rekey_row(f, wk, wi, s);  // t* below the last entry: every slot counts
                         const bool ht = wi != kNoIdx;
                         if (ro.idx != kNoIdx && !(ht && better(wk, wi, ro.key, ro.idx))) {
                             kf = 1;  // a first touch of a node no candidate list held
@@ -996,8 +1099,31 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                         const bool fo = fits(rc, rm, rp, sel, b0, b1, b2, lab, LAB);
                         const bool fn = fits(rc, rm, rp, sel, n0, n1, n2, lab, LAB);
                         fcc += (int32_t)fn - (int32_t)fo;
-                        const double kv =
-                            lane_key<PRIO, DOM, LAB, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, y3, pr);
+                        double kv;
+                        if constexpr (SCR) {  // the pods after f use this column
+                            const double nf0 = (double)n0, nf1 = (double)n1, nf2 = (double)n2;
+                            const double ny0 = recip_or_zero(n0, nf0), ny1 = recip_or_zero(n1, nf1),
+                                         ny2 = recip_or_zero(n2, nf2);
+                            bool lo;
+                            const float v = screen_pair(screen_req(rc), screen_req(rm), screen_req(rp), screen_y(n0, ny0),
+                                                        screen_y(n1, ny1), screen_y(n2, ny2), n0 >= rc, n1 >= rm, n2 >= rp,
+                                                        &lo);
+                            const bool need = lane > f && pj && !(v < m.thr[lane]);
+                            const bool any = __ballot(need) != 0;
+                            if (any) {
+                                const bool el = pair_key_fast<PRIO, DOM, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, nf0,
+                                                                              nf1, nf2, ny0, ny1, ny2, y3, pr, &kv);
+                                kv = el ? kv : -__builtin_inf();
+                            } else {
+                                kv = skip_key();
+                            }
+                            if (A.dbg && lane == 0) {  // diagnostics: sequential columns keyed, exactly
+                                atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[20]), 1ull);
+                                if (any) atomicAdd(reinterpret_cast<unsigned long long *>(&A.dbg[21]), 1ull);
+                            }
+                        } else {
+                            kv = lane_key<PRIO, DOM, LAB, F53>(fn, rc, rm, rp, rcf, rmf, rpf, n0, n1, n2, y3, pr);
+                        }
                         Srow[s] = kv;
                         if (lane == 0) {
                             SpcSlot &x = m.T[s];
@@ -1049,11 +1175,14 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             if (lane == 0) { m.ctl[0] = c; m.ctl[2] = (done < nb || c >= nb) ? 1 : 0; }
         }
         __syncthreads();
+        if (first && tr1) tr1[51] = wall_clock64();  // its check done
+        first = false;
         if (dbg) { const uint64_t t = __builtin_amdgcn_s_memtime(); t_s3 += t - t_mark; t_mark = t; }
         if (m.ctl[2]) break;
         c = m.ctl[0];
     }
     if (wave != 0) return true;
+    if (tr1) tr1[52] = wall_clock64();  // the rounds done
 
     auto store_out = [&]() {
         if (lane < done) {
@@ -1096,6 +1225,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             // no drain in front of the record: commit(b + 1) polls the record and the export's tagged chunks in
             // one round of loads (the plan reaches the score workgroups behind publish_committed's drain)
             put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
+            if (A.trace_row) A.trace_row[53] = wall_clock64();  // the hand-off record issued
         } else {
             A.xout->count = base;
             store_i64<COH>(&A.ctl->cursor, p0 + done);
@@ -1148,7 +1278,7 @@ template <int K, int NT = kSpcThreads, bool LAG3 = false>
 constexpr size_t spc_lds_bytes() {
     return (size_t)64 * (spc_slots<LAG3>() + 1) * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 +
            spc_slots<LAG3>() * sizeof(SpcSlot) + (size_t)kSpcHash * 4 + (size_t)K * 64 * 4 + 64 * 4 +
-           spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 2 + 64 * 64;
+           spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 4 + 64 * 2 + 64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
 // the prologue's aliases: the inherited snapshot states in D, their staged doubles in GS

@@ -544,8 +544,8 @@ int enqueue_batched(ksched_ctx *c) {
     Ctl *ctl = reinterpret_cast<Ctl *>(c->d_cursor);
     HIPCHK(c, launch_ctl_init(ctl, pl.B, c->p, 2, sS));
     for (int r = 0; r <= kRing; ++r) HIPCHK(c, hipMemsetAsync(xbuf(r == kRing ? -1 : r), 0, 8, sS));
-    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
-    if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), sS));
+    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 32 * sizeof(int64_t)));
+    if (c->d_dbg) HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 32 * sizeof(int64_t), sS));
     if (c->diag.merge_stamps && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));
     if (c->d_mdbg) HIPCHK(c, hipMemsetAsync(c->d_mdbg, 0, 8 * sizeof(int64_t), sS));
     HIPCHK(c, hipEventRecord(c->ev_pipe[0], sS));  // stream C starts after the initialisation above
@@ -734,8 +734,13 @@ void print_persist_trace(ksched_ctx *c) {
         }
     }
     if (c->d_dbg) {
-        int64_t hd[16];
-        if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14])
+        int64_t hd[32];
+        if (hipMemcpy(hd, c->d_dbg, sizeof(hd), hipMemcpyDeviceToHost) == hipSuccess && hd[14] && hd[16])
+            fprintf(stderr, "persist commit screen: export(b-1) entries %lld keyed exactly %.4f | guessed columns %lld, "
+                    "exactly %.4f | sequential columns %lld, exactly %.4f | rescue re-keys %lld\n", (long long)hd[16],
+                    (double)hd[17] / std::max<int64_t>(1, hd[16]), (long long)hd[18], (double)hd[19] / std::max<int64_t>(1, hd[18]),
+                    (long long)hd[20], (double)hd[21] / std::max<int64_t>(1, hd[20]), (long long)hd[22]);
+        if (hd[14])
             fprintf(stderr, "persist commit: batches=%lld rounds/batch %.3f guess iterations/round %.2f failures %lld | "
                     "cycles/batch: before the wait %.0f (other waves %.0f) entry to past the wait %.0f (poll %.0f, poll + barrier %.0f, early read sufficed %.3f) | prologue %.0f guess %.0f evaluate %.0f check %.0f total %.0f\n",
                     (long long)hd[14], (double)hd[12] / hd[14], (double)hd[5] / std::max<int64_t>(1, hd[12]),
@@ -911,9 +916,9 @@ int enqueue_persistent(ksched_ctx *c) {
         a.xdbg = c->d_xdbg;
         a.xdbg_cap = cap;
     }
-    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 16 * sizeof(int64_t)));
+    if (c->diag.commit_stamps && !c->d_dbg) HIPCHK(c, hipMalloc(&c->d_dbg, 32 * sizeof(int64_t)));
     if (c->d_dbg) {
-        HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 16 * sizeof(int64_t), c->stream));
+        HIPCHK(c, hipMemsetAsync(c->d_dbg, 0, 32 * sizeof(int64_t), c->stream));
         a.cdbg = c->d_dbg;
     }
     if (c->diag.merge_stamps && !c->d_mdbg) HIPCHK(c, hipMalloc(&c->d_mdbg, 8 * sizeof(int64_t)));

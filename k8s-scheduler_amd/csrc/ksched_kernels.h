@@ -573,7 +573,7 @@ hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hip
 // waves past), 24 before the wait, 25 entry -> past the wait, 26-30 the check step's split (update, probe, commit,
 // rescan, state load), 31-32 the guess step's (set-up, fixpoint), 33-36 the wave-0 state's (26-36: builds with
 // KSCHED_COMMIT_SPLIT only)
-constexpr int kTraceCols = 49;  // + 37-48: score WG 0's waves' pass-1 ends
+constexpr int kTraceCols = 54;  // + 37-48: score WG 0's waves' pass-1 ends; 49-53: the commit's rounds
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }

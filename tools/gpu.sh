@@ -65,6 +65,15 @@ case "$1" in
     abl base1 base && abl main1 main && abl base2 base && abl main2 main &&
     trace trace_c4
     ;;
+  full)  # a commit change: smoke, parity (persistent subset, full-size, exchange), screen counters, trace, bench
+    step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+    step pytest_pipe 600 $PYT tests/test_gpu_parity.py -k "persistent or golden or edge or full_size_c3" &&
+    step pytest_full 900 $PYT tests/test_gpu_fullsize.py &&
+    step pytest_xchg 900 $PYT tests/test_gpu_xchg.py &&
+    KSCHED_COMMIT_STAMPS=1 KSCHED_PERSIST_TRACE=1 step stamps_c4 300 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-check &&
+    trace trace_c4 &&
+    bench bench_c4
+    ;;
   xchg_exp)  # DESIGN 6.1's ring experiment
     soft xchg_exp 900 python -u tools/xchg_ring_experiment.py $XCHG_VARIANTS
     ;;

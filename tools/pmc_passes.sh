@@ -2,7 +2,7 @@
 # rocprofv3 kernel statistics and PMC passes of the default c4 bench itself (the binary and workload the bench
 # line times: one warm-up step + one timed step), one counter group per profiled run, each under its own kill
 # timer (MI355X_MICROARCH "rocprofv3 PMC slots": <= 8 SQ, <= 4 TCC -- FETCH_SIZE 3, WRITE_SIZE 2 -- per pass).
-#   bash tools/pmc_passes.sh <tag> stats|fetch|write|sq|sq2|all
+#   bash tools/pmc_passes.sh <tag> stats|fetch|write|sq|sq2|ic|list|all
 # Output: gpurun_out/pmc_<tag>/<pass>/run_*.csv; then
 #   python tools/pmc_summary.py profiles/<tag>_pmc_c4_pipe.json gpurun_out/pmc_<tag>/{fetch,write,sq,sq2}
 set -o pipefail
@@ -41,6 +41,9 @@ run() {
           SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE ;;
     sq2) pass sq2 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
            SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU ;;
+    ic) pass ic SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_WAIT_INST_ANY SQ_WAVE_CYCLES \
+          SQ_BUSY_CYCLES GRBM_GUI_ACTIVE ;;
+    list) timeout -s KILL 60 rocprofv3 -L > "$out/avail.txt" 2>&1; echo "list rc=$?" ;;
     all) run stats && run fetch && run write && run sq && run sq2 ;;
     *) echo "unknown pass $1"; return 2 ;;
   esac

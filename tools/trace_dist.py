@@ -9,7 +9,7 @@ import sys
 
 import numpy as np
 
-COLS = 49
+COLS = 54
 
 
 def main():
@@ -35,17 +35,35 @@ def main():
         ph["P1: past merges' wait -> past the hand-off"] = t[b, 22] - t[b, 3]
         ph["commit(b-1) end -> past the hand-off"] = t[b, 22] - t[b - 1, 4]
         ph["past the hand-off -> commit end"] = t[b, 4] - t[b, 22]
-        if (t[b, 25] > 0).all():
-            ph["  hand-off -> export(b-1) in slots"] = t[b, 23] - t[b, 22]
-            ph["  -> its keys"] = t[b, 24] - t[b, 23]
-            ph["  -> rounds start (wave-0 state)"] = t[b, 25] - t[b, 24]
-            ph["  rounds start -> commit end"] = t[b, 4] - t[b, 25]
+    sub = {}
+    bs = b[(t[b, 22] > 0) & (t[b, 23] > 0) & (t[b, 24] > 0) & (t[b, 25] > 0) & (t[b, 49] > 0) & (t[b, 53] > 0)
+           & (t[b - 1, 53] > 0) & ((t[b, 16] & 0xffff) == 1)]
+    if len(bs):  # single-round batches: the chain from commit(b-1)'s record to commit(b)'s
+        sub = {
+            "record(b-1) issued -> past the hand-off": t[bs, 22] - t[bs - 1, 53],
+            "  hand-off -> export(b-1) in slots": t[bs, 23] - t[bs, 22],
+            "  -> its keys": t[bs, 24] - t[bs, 23],
+            "  -> rounds start (wave-0 state)": t[bs, 25] - t[bs, 24],
+            "  -> guess done": t[bs, 49] - t[bs, 25],
+            "  -> evaluation done": t[bs, 50] - t[bs, 49],
+            "  -> check done": t[bs, 51] - t[bs, 50],
+            "  -> wave 0 past the rounds": t[bs, 52] - t[bs, 51],
+            "  -> record issued (export, plan)": t[bs, 53] - t[bs, 52],
+            "record(b-1) -> record(b)": t[bs, 53] - t[bs - 1, 53],
+            "record(b) -> commit end (publish, outputs)": t[bs, 4] - t[bs, 53],
+        }
     print(f"{len(b)} batches (lag {lag})")
     print(f"{'phase':48s} {'mean':>7s} {'p10':>7s} {'p50':>7s} {'p90':>7s} {'p99':>7s} {'max':>9s}  (us)")
     for k, v in ph.items():
         v = us(v.astype(np.float64))
         q = np.percentile(v, [10, 50, 90, 99])
         print(f"{k:48s} {v.mean():7.2f} {q[0]:7.2f} {q[1]:7.2f} {q[2]:7.2f} {q[3]:7.2f} {v.max():9.1f}")
+    if sub:
+        print(f"single-round batches ({len(bs)}), the commit chain:")
+        for k, v in sub.items():
+            v = us(v.astype(np.float64))
+            q = np.percentile(v, [10, 50, 90, 99])
+            print(f"{k:48s} {v.mean():7.2f} {q[0]:7.2f} {q[1]:7.2f} {q[2]:7.2f} {q[3]:7.2f} {v.max():9.1f}")
     per = us((t[b, 4] - t[b - 1, 4]).astype(np.float64))
     med = np.median(per)
     slow = per > 3 * med
@@ -73,15 +91,6 @@ def main():
         if s.any():
             print(f"  {r} rescues: {s.sum()} batches, commit mean {cm[s].mean():.1f} p50 {np.median(cm[s]):.1f} max {cm[s].max():.1f} us,"
                   f" rounds mean {rounds[s].mean():.2f}, resolved {done[s].mean():.1f}")
-    one = (cc & 0xffff) == 1
-    if one.any():
-        q = [t[b[one], c].mean() / 1e3 for c in (24, 25, 22, 23, 18)]
-        print(f"single-round batches, kcycles: before the wait {q[0]:.1f}, entry -> past the wait {q[1]:.1f}; after the wait:"
-              f" lists in + hashed {q[2]:.1f}, all waves past {q[3]:.1f}, prologue end {q[4]:.1f}")
-    if one.any():
-        q = [t[b[one], c].mean() / 1e3 for c in (33, 34, 35, 36)]
-        print(f"  wave-0 state, kcycles: fcc (list loads) {q[0]:.1f}, cut + list lengths {q[1]:.1f}, partial bests {q[2]:.1f},"
-              f" older export's best {q[3]:.1f}")
     print("commit time by rounds (kcycles per batch: prologue / guess / evaluate / check):")
     for lo, hi in ((0, 1), (1, 2), (2, 3), (3, 5), (5, 10), (10, 1 << 16)):
         s = (rounds >= lo) & (rounds < hi)

@@ -13,7 +13,7 @@ import sys
 
 import numpy as np
 
-COLS = 49
+COLS = 54
 LAG = 3
 
 
