@@ -24,7 +24,10 @@
 #include <hip/hip_runtime.h>
 
 #ifndef KSCHED_XCHG_DEBUG
-#define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tools/xchg_ring_experiment.py (a separate build)
+#define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tests/diag/xchg_ring_experiment.py (a separate build)
+#endif
+#ifndef KSCHED_NO_TOUCH_SCREEN
+#define KSCHED_NO_TOUCH_SCREEN 0  // A/B builds: every touched-node key exact
 #endif
 
 #include "ksched_kernels.h"
@@ -330,8 +333,8 @@ struct HandoffRes {
 struct NoHandoff {
     __device__ int operator()(HandoffRes *, XRec *) const { return 0; }
 };
-// commit(b)'s hand-off record for commit(b + 1) (one lane).  Its stores need not be drained first: both granules
-// and every chunk of the export it announces carry the tag, and commit(b + 1) polls them all
+// commit(b)'s hand-off record for commit(b + 1) (one lane), behind a drain of every store of commit(b): both granules
+// and every chunk of the export it announces carry the tag, and commit(b + 1) polls them all in one round of loads
 __device__ __forceinline__ void put_handoff(Ctl *ctl, int64_t batch, int n1, int64_t cursor, int64_t rseq, int64_t plan_next) {
     const __amdgpu_buffer_rsrc_t r = coh_rsrc(&ctl->hrec);
     const uint32_t tag = (uint32_t)(batch + 1);
@@ -349,7 +352,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     constexpr int kSpcWaves = NT / 64;
     constexpr int kSpcThreads = NT;
     constexpr bool LAG3 = COH;  // the persistent pipeline runs at lag kPipeLag = 3
-    constexpr bool SCR = COH && PRIO != kPrioPrice;  // the touched-node screen (above)
+    constexpr bool SCR = COH && PRIO != kPrioPrice && !KSCHED_NO_TOUCH_SCREEN;  // the touched-node screen (above)
     static_assert(!COH || kPipeLag == 3, "commit_spc_batch: the persistent pipeline's inheritance is lag 3");
     constexpr int kSpcRow = spc_slots<LAG3>() + 1;
     const int tid = threadIdx.x;
@@ -374,6 +377,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;
                     L->rseq = ho.rseq;
                     persist_plan(A, false, ho.cursor);
+                    drain_stores();  // every store of this commit lands before its hand-off record (below)
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
@@ -402,27 +406,30 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     uint64_t t_s1 = 0, t_s2 = 0, t_s3 = 0, t_mark = 0;
     SpcSmem m;
     {
+        // every array but S below 64 KB: an LDS instruction's immediate offset (16 bits) then reaches it from one
+        // per-lane (or per-index) address register -- with S first, each of the arrays above it needed an address
+        // register of its own, which the compiler hoisted out of the batch loop and spilled
         char *p = smem;
-        m.S = reinterpret_cast<double *>(p); p += (size_t)64 * kSpcRow * sizeof(double);
         m.pbk = reinterpret_cast<double *>(p); p += (size_t)kSpcWaves * 64 * sizeof(double);
         m.pbx = reinterpret_cast<int64_t *>(p); p += (size_t)kSpcWaves * 64 * sizeof(int64_t);
         m.LK = reinterpret_cast<double *>(p); p += (size_t)K * 64 * sizeof(double);
+        m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
+        m.D = reinterpret_cast<int8_t *>(p); p += 64 * 64;
         m.T = reinterpret_cast<SpcSlot *>(p); p += (size_t)spc_slots<LAG3>() * sizeof(SpcSlot);
-        m.hk = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
+        m.LI = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
         m.HP = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
+        m.hk = reinterpret_cast<int32_t *>(p); p += kSpcHash * sizeof(int32_t);
         m.tkc = reinterpret_cast<uint32_t *>(p); p += 64 * sizeof(uint32_t);
         m.ti = reinterpret_cast<int32_t *>(p); p += spc_slots<LAG3>() * sizeof(int32_t);
-        m.LI = reinterpret_cast<int32_t *>(p); p += (size_t)K * 64 * sizeof(int32_t);
         m.fcg = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.dfacc = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.gn = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.gq = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.gs = reinterpret_cast<int32_t *>(p); p += 64 * sizeof(int32_t);
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
-        m.GS = reinterpret_cast<uint64_t *>(p); p += 64 * kGS * sizeof(uint64_t);
         m.thr = reinterpret_cast<float *>(p); p += 64 * sizeof(float);
         m.x2s = reinterpret_cast<int16_t *>(p); p += 64 * sizeof(int16_t);
-        m.D = reinterpret_cast<int8_t *>(p);
+        m.S = reinterpret_cast<double *>(p);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
         m.s0 = reinterpret_cast<int64_t *>(m.D);
         m.iy = reinterpret_cast<double *>(m.GS);
@@ -443,10 +450,14 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     uint64_t w0[kHeadPer], w1[kHeadPer];
     int64_t fc0v = 0;
     int cut0 = 0;
+    int32_t thr0 = 0;  // SCR: the list's screen threshold as f32 bits (entry 1's pad)
     auto load_lists = [&]() {
         fc0v = (wave == 0 && pj) ? load_i64<COH>(A.fc0 + lane) : 0;
         cut0 = (wave == 0 && pj) ? (int32_t)(uint32_t)(load_i64<COH>(
                                        reinterpret_cast<const int64_t *>(A.lists + (size_t)lane * K) + 6) >> 32) : 0;
+        if (SCR)
+            thr0 = (wave == 0 && pj) ? (int32_t)(uint32_t)(load_i64<COH>(
+                                           reinterpret_cast<const int64_t *>(A.lists + (size_t)lane * K + 1) + 6) >> 32) : 0;
 #pragma unroll
         for (int u = 0; u < kHeadPer; ++u) {
             const int e = tid + u * kSpcThreads;
@@ -625,20 +636,9 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             const int i = tid + u * kSpcThreads;
             if (i < 64 * 64 && (i & 63) < n2 && (i >> 6) < nb) m.S[(size_t)(i >> 6) * kSpcRow + (i & 63)] = x2v[u];
         }
-        if constexpr (SCR) {  // the touched-node screen's thresholds (the hand-off's barrier publishes them)
-            __syncthreads();  // LK / LI complete
-            if (wave == 0) {
-                float t = -__builtin_inff();  // complete lists (and lanes past the batch): never skipped
-                if (pj && cut0) {
-                    int n = 0;  // the list length (valid entries form a prefix): a binary search
-#pragma unroll
-                    for (int st = K; st >= 1; st >>= 1)
-                        if (n + st <= K && m.LI[(n + st - 1) * 64 + lane] != kNoIdx) n += st;
-                    if (n > 0) t = (float)(m.LK[(n - 1) * 64 + lane] - 5e-5);
-                }
-                m.thr[lane] = t;
-            }
-        }
+        // the touched-node screen's thresholds: the mergers' (list_thr_bits, entry 1's pad); the hand-off's barrier
+        // publishes them
+        if (SCR && wave == 0) m.thr[lane] = (pj && A.touch_screen) ? __uint_as_float((uint32_t)thr0) : -__builtin_inff();
         // ---- the hand-off: commit(b - 1) published (a workgroup barrier) ----
         // (wave 0 lane e < n1 receives entry e of export(b - 1) with the record: the same round of loads)
         HandoffRes ho;
@@ -655,6 +655,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&A.ctl->stats[3]), 1ull,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     persist_plan(A, false, ho.cursor);
+                    drain_stores();  // every store of this commit lands before its hand-off record (below)
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
                 publish_committed<COH>(A);
@@ -1222,8 +1223,11 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
             L->cursor = p0 + done;
             persist_plan(A, done < nb, p0 + done);
-            // no drain in front of the record: commit(b + 1) polls the record and the export's tagged chunks in
-            // one round of loads (the plan reaches the score workgroups behind publish_committed's drain)
+            // every store of this commit -- the export, its {count, tag} header, the plan -- lands before the hand-off
+            // record: commit(b + 1) may publish Ctl::committed = b + 2 before this workgroup publishes b + 1, and a
+            // reader that sees b + 2 reads export(b) (round 5: without this drain a score workgroup could read the
+            // header before it landed and skip a whole export)
+            drain_stores();
             put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
             if (A.trace_row) A.trace_row[53] = wall_clock64();  // the hand-off record issued
         } else {
@@ -1274,6 +1278,12 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     return 1;
 }
 
+// the arrays in front of S (SpcSmem's layout in commit_spc_batch)
+template <int K, int NT = kSpcThreads, bool LAG3 = false>
+constexpr size_t spc_small_bytes() {
+    return (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 8 + 64 * kGS * 8 + 64 * 64 + spc_slots<LAG3>() * sizeof(SpcSlot) +
+           (size_t)K * 64 * 8 + (size_t)kSpcHash * 4 + 64 * 4 + spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * 4 + 64 * 2;
+}
 template <int K, int NT = kSpcThreads, bool LAG3 = false>
 constexpr size_t spc_lds_bytes() {
     return (size_t)64 * (spc_slots<LAG3>() + 1) * 8 + (size_t)(NT / 64) * 64 * 16 + (size_t)K * 64 * 12 +
@@ -1281,6 +1291,8 @@ constexpr size_t spc_lds_bytes() {
            spc_slots<LAG3>() * 4 + 5 * 64 * 4 + 16 + 64 * kGS * 8 + 64 * 4 + 64 * 2 + 64 * 64;
 }
 static_assert(spc_lds_bytes<16>() <= 160 * 1024, "k_commit_spc LDS");
+static_assert(spc_lds_bytes<16, kPipeThreads, true>() == spc_small_bytes<16, kPipeThreads, true>() + 64 * 193 * 8,
+              "SpcSmem: S last");
 // the prologue's aliases: the inherited snapshot states in D, their staged doubles in GS
 static_assert(64 * 64 >= 128 * 3 * 8 && 64 * kGS * 8 >= 128 * 6 * 8, "SpcSmem prologue aliases");
 static_assert((size_t)(kSpcThreads / 64) * 64 * 16 >= kSpcHash * 4 && (kPipeThreads / 64) * 64 * 16 >= kSpcHash * 4,

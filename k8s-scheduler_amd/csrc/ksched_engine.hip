@@ -206,6 +206,7 @@ struct ksched_ctx {
         int xchg_diag = 0;       // KSCHED_XCHG_DIAG (section 6.1's experiment): 1 ring zeroed by hipMemsetAsync, 2 local tags from 1
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
+        bool touch_screen = true;  // KSCHED_NO_TOUCH_SCREEN=1: the commit keys every touched node exactly
         int rescue_max = 4;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
                                  // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
                                  // (the budget table)
@@ -864,6 +865,7 @@ int enqueue_persistent(ksched_ctx *c) {
     // results through the rings (ksched_commit.h rescue_rank_fold)
     a.rescue = c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     a.rescue_max = c->diag.rescue_max;
+    a.touch_screen = c->diag.touch_screen ? 1 : 0;
     a.inh = reinterpret_cast<char *>(a.prog) + prog_b + resc_b;
     c->d_prog = a.prog;
     c->prog_G = G;
@@ -1084,6 +1086,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
     c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
+    c->diag.touch_screen = env_int("KSCHED_NO_TOUCH_SCREEN", 0) == 0;
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane

@@ -278,6 +278,7 @@ struct CommitArgs {
     char *rescue;           // persistent pipeline: the rescue request / results (else null: truncate)
     int32_t rescue_n;       // merger slots serving a rescue (= B)
     int32_t rescue_max;     // rescues per batch; the next exhausted list truncates the batch
+    int32_t touch_screen;   // persistent commit: the touched-node screen on (KSCHED_NO_TOUCH_SCREEN=1 turns it off)
     const char *inh;        // persistent commit: the mergers' keys of the older export (inherit_x2_keys), else null
     int64_t timeout_ticks;  // bound of the rescue wait
     int32_t *err;           // device error word (12 = the rescue wait timed out)
@@ -314,13 +315,17 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __hip_atomic_store(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (COH)  // two commit workgroups: a maximum, so the count never steps back when b + 1 lands after b + 2
+            __hip_atomic_fetch_max(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_store(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
-    // persistent pipeline: the per-XCD replicas (lanes 0..7 of the publishing wave, one store each)
+    // persistent pipeline: the per-XCD replicas (lanes 0..7 of the publishing wave, one each)
     if (COH && (threadIdx.x & 63) < kCtlReplicas)
-        __hip_atomic_store(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // every replica of Ctl::committed (the persistent pipeline's end and error paths; lanes 0..7)
 __device__ __forceinline__ void publish_committed_all(Ctl *ctl, unsigned long long v) {
@@ -473,6 +478,7 @@ struct PersistArgs {
     char *rescue;           // this rank's RescueReq + Rec res[B] (null: exhausted lists truncate their batch)
     int32_t poison_lds;     // diagnostics (KSCHED_POISON): bytes of dynamic LDS every workgroup fills with 0xff first
     int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
+    int32_t touch_screen;   // the commit's touched-node screen (KSCHED_NO_TOUCH_SCREEN=1: every key exact)
     // the merger slots' keys of their pod against the entries of export(b - 2), which commit(b) inherits:
     // [4 batches][B] summaries {sum of predicate deltas, best key, best idx | entry << 32, -} then [4][B][64] keys
     char *inh;

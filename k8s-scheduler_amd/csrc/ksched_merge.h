@@ -279,6 +279,19 @@ __device__ __forceinline__ int wave_rank(uint64_t code, int32_t idx, uint64_t mc
     return r;
 }
 
+// The touched-node screen's threshold of a merged list (lane = output entry; okm: the valid entries, a prefix;
+// mc: this lane's key code): RN_f32(last key - 5e-5) when the list is cut, -inf otherwise, as f32 bits.
+__device__ __forceinline__ int32_t list_thr_bits(bool cut, uint64_t okm, uint64_t mc) {
+    const int nv = __popcll(okm);
+    float t = -__builtin_inff();
+    if (cut && nv > 0) {
+        const uint64_t c = readlane_u64(mc, nv - 1);
+        const uint64_t u = (c >> 63) ? (c & 0x7fffffffffffffffull) : ~c;  // inverse of key_code
+        t = (float)(__longlong_as_double((long long)u) - 5e-5);
+    }
+    return (int32_t)__float_as_uint(t);
+}
+
 __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -422,11 +435,14 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     // lists outside the kept K, or entries beyond K, remain: the output is cut
     const bool left = ntot > nkeep || nvalid > K;
     const int32_t cut_out = (gcut || left) ? 1 : 0;
+    const uint64_t mc = sm.ocode[lane < nout ? lane : 0];
+    const int32_t mi = sm.oidx[lane < nout ? lane : 0];
+    const bool ok = lane < K && lane < nout && !(gi != kNoIdx && code_better(gk, gi, mc, mi));
+    // the commit's touched-node threshold (ksched_commit.h, kSkipKeyBits) in entry 1's pad: the last entry's key
+    // - 5e-5 as an f32 below it, for a cut list; -inf (never skip) for a complete one
+    const int32_t thr_bits = list_thr_bits(cut_out != 0, __ballot(ok), mc);
     if (lane < K) {
         Rec r{};
-        const uint64_t mc = sm.ocode[lane < nout ? lane : 0];
-        const int32_t mi = sm.oidx[lane < nout ? lane : 0];
-        const bool ok = lane < nout && !(gi != kNoIdx && code_better(gk, gi, mc, mi));
         if (ok) {
             const NodeRec &nd = A.nodes[mi - A.node_offset];
             const uint64_t u = (mc >> 63) ? (mc & 0x7fffffffffffffffull) : ~mc;  // inverse of key_code
@@ -436,7 +452,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         } else {
             r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
         }
-        r.pad = lane == 0 ? cut_out : 0;
+        r.pad = lane == 0 ? cut_out : (lane == 1 ? thr_bits : 0);
         if (A.lds_msg) {
             const uint32_t *w = reinterpret_cast<const uint32_t *>(&r);
 #pragma unroll

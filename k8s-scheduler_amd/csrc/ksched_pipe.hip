@@ -148,6 +148,7 @@ __device__ __forceinline__ void rank_merge_msgs(const uint32_t *all, int R, Rec 
     const bool left = __ballot(h < n) != 0;
     if (anycut && mi != kNoIdx && better(ck, ci, mk, mi)) { mk = -__builtin_inf(); mi = kNoIdx; }
     const int32_t cut_out = (anycut || left) ? 1 : 0;
+    const int32_t thr_bits = list_thr_bits(cut_out != 0, __ballot(lane < K && mi != kNoIdx), key_code(mk));
     if (lane < K) {
         Rec r{};
         if (mi != kNoIdx) {
@@ -158,7 +159,7 @@ __device__ __forceinline__ void rank_merge_msgs(const uint32_t *all, int R, Rec 
         } else {
             r.key = -__builtin_inf(); r.idx = kNoIdx; r.valid = 0;
         }
-        r.pad = lane == 0 ? cut_out : 0;
+        r.pad = lane == 0 ? cut_out : (lane == 1 ? thr_bits : 0);  // entry 1: the screen threshold (list_thr_bits)
         store_rec<true>(out + lane, r);
     }
     if (lane == 0) store_i64<true>(out_fc, cnt);
@@ -176,7 +177,7 @@ __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int
 // row u of the step goes to slot u % KC, which keeps the MAXIMUM of its rows (one v_max per pair instead of
 // an insertion into a sorted list): the KC slots of a wave, and of the 12 waves, are lower bounds of keys of
 // DISTINCT rows, so the KC-th largest of them is at most the KC-th largest key of the workgroup -- a valid
-// L, at most slightly weaker than the KC-th largest of all the rows' bounds (tools/screen_sim.py: c4 exact
+// L, at most slightly weaker than the KC-th largest of all the rows' bounds (tests/diag/screen_sim.py: c4 exact
 // rows +4 %).  Otherwise a sorted top-KC insertion.
 #ifndef KSCHED_SCORE_PREFETCH
 #define KSCHED_SCORE_PREFETCH 1
@@ -322,6 +323,9 @@ constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 
 template <int K>
 constexpr size_t commit_total_bytes() { return commit_loc_bytes() + spc_lds_bytes<K, kPipeThreads, true>(); }
 static_assert(commit_total_bytes<16>() <= 160 * 1024, "the persistent commit's LDS (lag-3 slots)");
+// (+ 256: the kernel's static LDS, placed in front of the dynamic block)
+static_assert(commit_loc_bytes() + spc_small_bytes<16, kPipeThreads, true>() + 256 <= 65536,
+              "the persistent commit's arrays in front of S reach LDS immediate offsets");
 
 // ------------------------------------------------------------------------------------------------
 // SCORE role (waves 0 .. kSW-1 of workgroup 1 + g)
@@ -1165,7 +1169,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
                 if (!ok) { set_err(P.err, 10); pc->m_stop = 1; }
                 sync();
                 if (pc->m_stop) return;
-#if KSCHED_XCHG_DEBUG  // diagnostics build (tools/xchg_ring_experiment.py): message hashes and the first messages
+#if KSCHED_XCHG_DEBUG  // diagnostics build (tests/diag/xchg_ring_experiment.py): message hashes and the first messages
                 if (P.xdbg && mtid <= RR && nact - 1 < P.xdbg_cap) {  // diagnostics: the messages as received / sent
                     const uint32_t *msg = mtid < RR ? s_all + mtid * MW : s_msg;
                     uint64_t h = 0x9e3779b97f4a7c15ull;
@@ -1369,6 +1373,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         ca.dbg_act = nact - 1;
         ca.rescue_n = P.B;
         ca.rescue_max = P.rescue_max;
+        ca.touch_screen = P.touch_screen;
         ca.inh = P.inh;
         ca.timeout_ticks = P.timeout_ticks;
         ca.err = P.err;

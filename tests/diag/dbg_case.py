@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Debug helper: one configuration against the oracle, first mismatches and the engine's stats.
 
-  python tools/dbg_case.py <config> <nodes> <pods> [wgs=0] [ranks=1]
+  python tests/diag/dbg_case.py <config> <nodes> <pods> [wgs=0] [ranks=1]
 ranks > 1: a local exchange group (threads of this process, ksched_xchg_join_local).  Environment variables
 of the engine (KSCHED_NO_SCREEN, KSCHED_DEBUG, ...) apply as usual."""
 import os
@@ -10,7 +10,7 @@ import threading
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd"), os.path.join(ROOT, "oracle")]
 
 

@@ -4,7 +4,7 @@ GPU workload and, at Python exit (before the C-level exit handlers run, every li
 writes /proc/self/maps to gpurun_out/maps_<variant>.txt so the addresses of a crash report can be mapped to
 their libraries.
 
-  rocprofv3 --kernel-trace --stats -d gpurun_out/prof_<v> -o run -- python3 tools/exit_probe.py <v>
+  rocprofv3 --kernel-trace --stats -d gpurun_out/prof_<v> -o run -- python3 tests/diag/exit_probe.py <v>
 variants: torch   torch only (one kernel)
           ksched  + libksched: one small batched schedule, context destroyed explicitly
           leak    + libksched: the same, context left to the interpreter's teardown
@@ -21,7 +21,7 @@ import atexit
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd"), os.path.join(ROOT, "oracle")]
 
 

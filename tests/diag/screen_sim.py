@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """CPU simulation of the screened scan's row counts on the real states of a run.
 
-  python tools/screen_sim.py c4 [G=255] [eps=1e-4] [t0,t1,...]
+  python tests/diag/screen_sim.py c4 [G=255] [eps=1e-4] [t0,t1,...]
 
 The node state before pod t is the initial state minus every placement of pods < t (the sequential
 schedule, from the CPU oracle -- cached in /tmp/screen_sim_<cfg>_idx.npy; the full c4 run takes ~6 min
@@ -16,7 +16,7 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "k8s-scheduler_amd"), os.path.join(ROOT, "oracle")]
 
 

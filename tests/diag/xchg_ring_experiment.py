@@ -5,7 +5,7 @@ group checked against the oracle.  Variants change one thing at a time: the ring
 (KSCHED_XCHG_DIAG=1: hipMemsetAsync as in round 4), whether tags restart at 1 (KSCHED_XCHG_DIAG=2), the history
 (the last group alone), poisoned workspace and LDS (KSCHED_POISON), the screened scan (KSCHED_NO_SCREEN).
 
-  python tools/xchg_ring_experiment.py [variant ...]     (one subprocess per variant; default: all)
+  python tests/diag/xchg_ring_experiment.py [variant ...]     (one subprocess per variant; default: all)
 
 The *_dump variants need the diagnostics build (the device-side dumps are compiled out of the product):
   bash tools/build_variant.sh xdbg "-DKSCHED_XCHG_DEBUG=1"     -> k8s-scheduler_amd/libksched_xdbg.so
@@ -15,7 +15,7 @@ import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SEQ = (("c3", 24000, 3000, 2), ("c4", 30000, 2500, 3), ("c4", 100000, 2500, 2))
 XDBG = {"KSCHED_LIB": os.path.join(ROOT, "k8s-scheduler_amd", "libksched_xdbg.so")}
 VARIANTS = {

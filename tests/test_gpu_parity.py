@@ -50,6 +50,24 @@ def assert_same(got, want, label=""):
         assert np.array_equal(a, b), f"{label}: final node state differs"
 
 
+def check_same(cl, mode, want, label, **kw):
+    """run_engine + assert_same; on a mismatch the case runs twice more -- as is, and with the commit's touched-node
+    screen off (KSCHED_NO_TOUCH_SCREEN=1) -- and the message says which of those matched (a rare mismatch then
+    names its cause: one that does not repeat, or the screen)."""
+    got = run_engine(cl, mode, **kw)
+    try:
+        assert_same(got, want, label)
+    except AssertionError as ex:
+        again = run_engine(cl, mode, **kw)
+        os.environ["KSCHED_NO_TOUCH_SCREEN"] = "1"
+        try:
+            off = run_engine(cl, mode, **kw)
+        finally:
+            del os.environ["KSCHED_NO_TOUCH_SCREEN"]
+        same = lambda g: bool(np.array_equal(g[0], want[0]))  # noqa: E731
+        raise AssertionError(f"{ex} | stats {got[4]} | again: matches {same(again)}, screen off: matches {same(off)}")
+
+
 def golden():
     with open(os.path.join(GOLDEN, "clusters.json")) as f:
         return json.load(f)
@@ -84,7 +102,7 @@ def test_edge_clusters_all_modes(gpu_available, oracle_mod, seed):
     cl = cluster.random_small(500 + seed, n_nodes=37 + 61 * seed, n_pods=700, priority=pr, domain=dm, use_labels=lb)
     want = oracle_mod.schedule(cl)
     for name, mode, kw in modes():
-        assert_same(run_engine(cl, mode, **kw), want, f"seed{seed}/{name}")
+        check_same(cl, mode, want, f"seed{seed}/{name}", **kw)
 
 
 @pytest.mark.parametrize("name,nn,pp", [("c2", 5000, 2000), ("c3", 20000, 1500), ("c5", 30000, 1500)])
@@ -93,7 +111,7 @@ def test_config_prefix_parity(gpu_available, oracle_mod, name, nn, pp):
     cl = cluster.make_cluster(name, n_nodes=nn, n_pods=pp)
     want = oracle_mod.schedule(cl, nthreads=8)
     for mname, mode, kw in modes():
-        assert_same(run_engine(cl, mode, **kw), want, f"{name}/{mname}")
+        check_same(cl, mode, want, f"{name}/{mname}", **kw)
 
 
 @pytest.mark.parametrize("kc", [2, 4, 16])

@@ -74,8 +74,18 @@ case "$1" in
     trace trace_c4 &&
     bench bench_c4
     ;;
+  full_ab)  # full's checks (failures reported, not fatal), then an A/B of the tree against two builds
+    step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+    soft pytest_pipe 600 $PYT tests/test_gpu_parity.py -k "persistent or golden or edge or full_size_c3" &&
+    soft pytest_full 900 $PYT tests/test_gpu_fullsize.py &&
+    soft pytest_xchg 900 $PYT tests/test_gpu_xchg.py &&
+    KSCHED_COMMIT_STAMPS=1 KSCHED_PERSIST_TRACE=1 step stamps_c4 300 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-check &&
+    trace trace_c4 &&
+    abl main1 main && abl ${AB1:-base}1 ${AB1:-base} && abl ${AB2:-noscr}1 ${AB2:-noscr} &&
+    abl main2 main && abl ${AB1:-base}2 ${AB1:-base} && abl ${AB2:-noscr}2 ${AB2:-noscr}
+    ;;
   xchg_exp)  # DESIGN 6.1's ring experiment
-    soft xchg_exp 900 python -u tools/xchg_ring_experiment.py $XCHG_VARIANTS
+    soft xchg_exp 900 python -u tests/diag/xchg_ring_experiment.py $XCHG_VARIANTS
     ;;
   all)
     step pytest_all 1100 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/
