@@ -26,6 +26,12 @@
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tests/diag/xchg_ring_experiment.py (a separate build)
 #endif
+#ifndef KSCHED_AB_NO_DRAIN
+#define KSCHED_AB_NO_DRAIN 0  // A/B builds only
+#endif
+#ifndef KSCHED_AB_S_FIRST
+#define KSCHED_AB_S_FIRST 0  // A/B builds only: the key matrix first in the commit's LDS (round 4's order)
+#endif
 #ifndef KSCHED_NO_TOUCH_SCREEN
 #define KSCHED_NO_TOUCH_SCREEN 0  // A/B builds: every touched-node key exact
 #endif
@@ -410,6 +416,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         // per-lane (or per-index) address register -- with S first, each of the arrays above it needed an address
         // register of its own, which the compiler hoisted out of the batch loop and spilled
         char *p = smem;
+        if (KSCHED_AB_S_FIRST) p += (size_t)64 * kSpcRow * sizeof(double);
         m.pbk = reinterpret_cast<double *>(p); p += (size_t)kSpcWaves * 64 * sizeof(double);
         m.pbx = reinterpret_cast<int64_t *>(p); p += (size_t)kSpcWaves * 64 * sizeof(int64_t);
         m.LK = reinterpret_cast<double *>(p); p += (size_t)K * 64 * sizeof(double);
@@ -429,7 +436,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
         m.thr = reinterpret_cast<float *>(p); p += 64 * sizeof(float);
         m.x2s = reinterpret_cast<int16_t *>(p); p += 64 * sizeof(int16_t);
-        m.S = reinterpret_cast<double *>(p);
+        m.S = KSCHED_AB_S_FIRST ? reinterpret_cast<double *>(smem) : reinterpret_cast<double *>(p);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
         m.s0 = reinterpret_cast<int64_t *>(m.D);
         m.iy = reinterpret_cast<double *>(m.GS);
@@ -641,6 +648,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         if (SCR && wave == 0) m.thr[lane] = (pj && A.touch_screen) ? __uint_as_float((uint32_t)thr0) : -__builtin_inff();
         // ---- the hand-off: commit(b - 1) published (a workgroup barrier) ----
         // (wave 0 lane e < n1 receives entry e of export(b - 1) with the record: the same round of loads)
+        if (A.xp) jitter_at(A.xp->jitter, A.batch, 103);  // P1 done late
         HandoffRes ho;
         const int hr = handoff(&ho, &xi);
         if (hr != 0) return hr < 0 ? 0 : 2;  // timed out / the end of the call (or another workgroup's error)
@@ -709,6 +717,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     int32_t rbi = kNoIdx, rbs = -1;
     int cv = 0, cut = 0;      // list length, cut flag
     int32_t my_idx = 0, my_feas = 0;
+    int32_t my_src = 0;  // diagnostics: the path that set my_idx (reported with device error 14)
     double my_score = 0.0;
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
     int nT = nin, done = nb, W = 64;
@@ -793,7 +802,11 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             // (cend - c) + 1 iterations and equals the sequential greedy guess order; with first touches
             // the rule (99 %), it is reached after two.  The entries' table positions and the mask of those
             // not confirmed-taken are loaded once per round; an iteration probes own[] only.
+            // own[] aliases pbk / pbx, which the wave-0 state (or the last check) just read as doubles: an LDS order
+            // on both sides of its initialisation, so no load or store moves across it (the accesses differ in type)
+            lds_order();
             for (int w = lane * 4; w < kSpcHash; w += 256) *reinterpret_cast<int4 *>(m.own + w) = make_int4(64, 64, 64, 64);
+            lds_order();
             const uint64_t fitm = __ballot(fcc != 0);  // pods with a feasible node before this round
             const bool act = lane >= c && lane < cend && ((fitm >> lane) & 1);
             int32_t hp[K];
@@ -978,6 +991,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             const bool conf = lane >= c && lane < f;
             if (conf) {
                 my_idx = kind == 1 ? my_g : (fcj == 0 ? -1 : -2);
+                my_src = 1 + kind + 8 * my_q;
                 my_score = kind == 1 ? (PRIO == kPrioPrice ? 0.0 - uk : uk) : 0.0;
                 my_feas = fcj;
                 if (guessed_commit) atomicOr(&m.tkc[my_h >> 5], 1u << (my_h & 31));
@@ -1076,6 +1090,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                 } else {
                     if (lane == f) {
                         my_idx = kf == 0 ? (fcf == 0 ? -1 : -2) : wi;
+                        my_src = 1000 + kf + (rescued ? 10 : 0) + 100 * (qf + 1) + 10000 * (int)(nseq & 63);
                         my_score = kf == 0 ? 0.0 : (PRIO == kPrioPrice ? 0.0 - wk : wk);
                         my_feas = fcf;
                     }
@@ -1186,6 +1201,19 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     if (tr1) tr1[52] = wall_clock64();  // the rounds done
 
     auto store_out = [&]() {
+        // an index no path of the commit can produce (a node index is < 2^30) is a device error, never an output
+        const bool bad_out = COH && lane < done && (my_idx < -2 || my_idx >= (1 << 30));
+        const uint64_t bm = __ballot(bad_out);
+        if (bm) {
+            const int l = (int)__builtin_ctzll(bm);
+            const int src = __builtin_amdgcn_readlane(my_src, l);
+            const int val = __builtin_amdgcn_readlane(my_idx, l);
+            if (lane == 0 && atomicCAS(A.err, 0, 14) == 0 && A.xp && A.xp->prog) {  // the words the host reports
+                A.xp->prog[kProgWords * (A.xp->G + A.xp->B) + 3] =
+                    (uint64_t)A.batch << 40 | (uint64_t)l << 32 | (uint64_t)(uint32_t)src;
+                A.xp->prog[kProgWords * (A.xp->G + A.xp->B) + 4] = (uint64_t)(uint32_t)val;
+            }
+        }
         if (lane < done) {
             A.out.idx[p0 + lane] = my_idx;
             A.out.score[p0 + lane] = my_score;
@@ -1227,7 +1255,8 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             // record: commit(b + 1) may publish Ctl::committed = b + 2 before this workgroup publishes b + 1, and a
             // reader that sees b + 2 reads export(b) (round 5: without this drain a score workgroup could read the
             // header before it landed and skip a whole export)
-            drain_stores();
+            if (!KSCHED_AB_NO_DRAIN) drain_stores();
+            if (A.xp) jitter_at(A.xp->jitter, A.batch, 101);
             put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
             if (A.trace_row) A.trace_row[53] = wall_clock64();  // the hand-off record issued
         } else {
@@ -1259,6 +1288,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             A.dbg[6] += t_pre;
         }
     }
+    if (COH && A.xp) jitter_at(A.xp->jitter, A.batch, 102);
     publish_committed<COH>(A);  // wave 0 made every global store of this batch
     if (COH) {
         // persistent pipeline: the outputs, the cursor and the counters are read by the host after the kernel

@@ -141,6 +141,7 @@ struct ksched_ctx {
     int64_t *d_cursor = nullptr;  // [0] cursor, [1..3] stats
     int64_t *h_cursor = nullptr;  // pinned
     int64_t *d_dbg = nullptr;     // KSCHED_COMMIT_STAMPS diagnostics
+    uint32_t jitter_calls = 0;    // KSCHED_JITTER: calls so far (the seed changes per call)
     int64_t *d_mdbg = nullptr;    // KSCHED_MERGE_STAMPS diagnostics
     hipStream_t stream2 = nullptr;  // merge + commit stream of the batched pipeline
     hipEvent_t ev_lists[4] = {}, ev_commit[4] = {}, ev_scored[4] = {}, ev_pipe[3] = {};
@@ -206,6 +207,7 @@ struct ksched_ctx {
         int xchg_diag = 0;       // KSCHED_XCHG_DIAG (section 6.1's experiment): 1 ring zeroed by hipMemsetAsync, 2 local tags from 1
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
+        uint32_t jitter = 0;     // KSCHED_JITTER=<seed>: random delays at the persistent pipeline's protocol points
         bool touch_screen = true;  // KSCHED_NO_TOUCH_SCREEN=1: the commit keys every touched node exactly
         int rescue_max = 4;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
                                  // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
@@ -866,6 +868,7 @@ int enqueue_persistent(ksched_ctx *c) {
     a.rescue = c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     a.rescue_max = c->diag.rescue_max;
     a.touch_screen = c->diag.touch_screen ? 1 : 0;
+    if (c->diag.jitter) a.jitter = c->diag.jitter * 2654435761u + (uint32_t)(++c->jitter_calls) * 40503u + 1u;
     a.inh = reinterpret_cast<char *>(a.prog) + prog_b + resc_b;
     c->d_prog = a.prog;
     c->prog_G = G;
@@ -932,6 +935,13 @@ int enqueue_persistent(ksched_ctx *c) {
     if (c->diag.poison) {  // read-before-write hunting: stale workspace and LDS become 0xff everywhere
         HIPCHK(c, hipMemsetAsync(c->d_pws, 0xff, need, sS));
         a.poison_lds = (int32_t)info.lds;
+        a.lds_fill = ~0u; a.lds_fill_role = 7; a.lds_fill_lo = 0; a.lds_fill_hi = (int32_t)info.lds;
+    } else if (const char *f = std::getenv("KSCHED_LDS_FILL"); f && *f) {  // LDS only, a chosen pattern and range
+        a.poison_lds = (int32_t)info.lds;
+        a.lds_fill = (uint32_t)std::strtoul(f, nullptr, 0);
+        a.lds_fill_role = env_int("KSCHED_LDS_ROLE", 7);
+        a.lds_fill_lo = env_int("KSCHED_LDS_LO", 0);
+        a.lds_fill_hi = env_int("KSCHED_LDS_HI", (int)info.lds);
     }
     HIPCHK(c, launch_ctl_init(a.ctl, B, c->p, kPipeLag, sS));
     // the export ring whole: its records carry batch tags (store_xrec), which an earlier call's must never match
@@ -1087,6 +1097,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
     c->diag.touch_screen = env_int("KSCHED_NO_TOUCH_SCREEN", 0) == 0;
+    c->diag.jitter = (uint32_t)env_int("KSCHED_JITTER", 0);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);
     c->diag.exchange_timeout_ms = env_int("KSCHED_EXCHANGE_TIMEOUT_MS", 2000);
     // KSCHED_COMMIT_LANE_PER_POD (round 1) is retired: accepted as the speculative commit  // touched table: 2B <= 256 = 4 slots per lane
@@ -1873,6 +1884,38 @@ static int sync_impl(ksched_ctx *c) {
         (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
         return fail(c, KSCHED_E_DEVICE, e == 2 ? "batched mode: the merge's wait for the score workgroups timed out"
                                                : "batched mode: the score's wait for commit(b-2) timed out");
+    }
+    if (e == 15) {
+        std::vector<uint64_t> w((size_t)(c->prog_G + c->prog_B + kCommitWGs) * kProgWords);
+        uint64_t where = 0;
+        if (!w.empty() && hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess)
+            for (int i = c->prog_G + c->prog_B; i < c->prog_G + c->prog_B + 2; ++i) where |= w[(size_t)kProgWords * i + 2];
+        (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
+        char buf[200];
+        snprintf(buf, sizeof buf, "persistent pipeline: the commit's LDS canary changed (batch %llu, word %llu, low bits %#llx)",
+                 (unsigned long long)(where >> 32), (unsigned long long)((where >> 16) & 0xffff),
+                 (unsigned long long)(where & 0xffff));
+        return fail(c, KSCHED_E_DEVICE, buf);
+    }
+    if (e == 14) {
+        std::vector<uint64_t> w((size_t)(c->prog_G + c->prog_B + kCommitWGs) * kProgWords);
+        uint64_t d = 0, v = 0;
+        if (hipMemcpy(w.data(), c->d_prog, w.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+            d = w[(size_t)kProgWords * (c->prog_G + c->prog_B) + 3];
+            v = w[(size_t)kProgWords * (c->prog_G + c->prog_B) + 4];
+        }
+        (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
+        char buf[240];
+        snprintf(buf, sizeof buf, "persistent pipeline: the commit produced a node index outside every node (%#llx; batch %llu, "
+                 "pod lane %llu, path %llu; a device protocol error, results discarded)", (unsigned long long)v,
+                 (unsigned long long)(d >> 40), (unsigned long long)((d >> 32) & 0xff), (unsigned long long)(d & 0xffffffffu));
+        return fail(c, KSCHED_E_DEVICE, buf);
+    }
+    if (e == 12 || e == 14) {
+        (void)hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream);
+        return fail(c, KSCHED_E_DEVICE, e == 12 ? "persistent pipeline: the commit's wait for a rescue timed out"
+                                                : "persistent pipeline: the commit produced a node index outside every "
+                                                  "node (a device protocol error; results discarded)");
     }
     if (e) return fail(c, KSCHED_E_DEVICE, "exact mode: cross-workgroup exchange timed out (workgroups not co-resident?)");
     return KSCHED_OK;

@@ -12,6 +12,9 @@
 // are bit-identical to hipcc's f64 division for this path's operands.
 // See DESIGN.md for the correctness argument of the batched commit.
 #pragma once
+#ifndef KSCHED_AB_PUBLISH_STORE
+#define KSCHED_AB_PUBLISH_STORE 0  // A/B builds only
+#endif
 
 #include "ksched_device.h"
 
@@ -315,7 +318,7 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (COH)  // two commit workgroups: a maximum, so the count never steps back when b + 1 lands after b + 2
+        if (COH && !KSCHED_AB_PUBLISH_STORE)  // two commit workgroups: a maximum, so the count never steps back
             __hip_atomic_fetch_max(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         else
@@ -323,9 +326,14 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     // persistent pipeline: the per-XCD replicas (lanes 0..7 of the publishing wave, one each)
-    if (COH && (threadIdx.x & 63) < kCtlReplicas)
-        __hip_atomic_fetch_max(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
+    if (COH && (threadIdx.x & 63) < kCtlReplicas) {
+        if (KSCHED_AB_PUBLISH_STORE)
+            __hip_atomic_store(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            __hip_atomic_fetch_max(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 // every replica of Ctl::committed (the persistent pipeline's end and error paths; lanes 0..7)
 __device__ __forceinline__ void publish_committed_all(Ctl *ctl, unsigned long long v) {
@@ -477,6 +485,10 @@ struct PersistArgs {
     uint64_t *prog;
     char *rescue;           // this rank's RescueReq + Rec res[B] (null: exhausted lists truncate their batch)
     int32_t poison_lds;     // diagnostics (KSCHED_POISON): bytes of dynamic LDS every workgroup fills with 0xff first
+    uint32_t lds_fill;      // diagnostics (KSCHED_LDS_FILL): the fill pattern (KSCHED_POISON: 0xffffffff)
+    int32_t lds_fill_role;  // roles filled: 1 commit, 2 score, 4 merge (KSCHED_LDS_ROLE, default all)
+    int32_t lds_fill_lo, lds_fill_hi;  // byte range filled (KSCHED_LDS_LO / KSCHED_LDS_HI)
+    uint32_t jitter;        // diagnostics (KSCHED_JITTER): seed of the random delays at the protocol points, 0 = off
     int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
     int32_t touch_screen;   // the commit's touched-node screen (KSCHED_NO_TOUCH_SCREEN=1: every key exact)
     // the merger slots' keys of their pod against the entries of export(b - 2), which commit(b) inherits:
@@ -580,6 +592,16 @@ hipError_t launch_xchg_min(const PersistArgs &a, int32_t mine, int32_t *out, hip
 // rescan, state load), 31-32 the guess step's (set-up, fixpoint), 33-36 the wave-0 state's (26-36: builds with
 // KSCHED_COMMIT_SPLIT only)
 constexpr int kTraceCols = 54;  // + 37-48: score WG 0's waves' pass-1 ends; 49-53: the commit's rounds
+// KSCHED_JITTER (race hunting): at one in four (workgroup, batch, site) triples, sleep the wave for up to ~50 us,
+// chosen by a hash of the seed -- a protocol that depends on timing then fails often instead of rarely
+__device__ __forceinline__ void jitter_at(uint32_t seed, int64_t b, int site) {
+    if (!seed) return;
+    uint32_t h = seed ^ (uint32_t)((uint64_t)b * 0x9E3779B1u) ^ ((uint32_t)site * 0x85EBCA77u) ^ (blockIdx.x * 0xC2B2AE3Du);
+    h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+    if ((h & 3) != 0) return;
+    const int n = (int)((h >> 8) & 255);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(8);
+}
 __device__ __forceinline__ void trace_at(const PersistArgs &P, int64_t b, int col) {
     if (P.trace && b < P.trace_cap) P.trace[b * kTraceCols + col] = wall_clock64();
 }

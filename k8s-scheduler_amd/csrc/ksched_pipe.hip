@@ -319,7 +319,9 @@ struct MergeLayout {
 };
 static_assert(sizeof(MergeCtl) <= 64, "MergeCtl");
 
-constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16; }
+// + kCanaryBytes between the control state and the commit's arrays (KSCHED_CANARY: checked every batch)
+constexpr size_t kCanaryBytes = 128;
+constexpr size_t commit_loc_bytes() { return (sizeof(PersistLocal) + 15) / 16 * 16 + kCanaryBytes; }
 template <int K>
 constexpr size_t commit_total_bytes() { return commit_loc_bytes() + spc_lds_bytes<K, kPipeThreads, true>(); }
 static_assert(commit_total_bytes<16>() <= 160 * 1024, "the persistent commit's LDS (lag-3 slots)");
@@ -436,6 +438,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 }
             } else {
                 int stop = 0;
+                jitter_at(P.jitter, b, 1);  // the score workgroup's wait and loads
                 if (lane == 0) {
                     unsigned long long seen = 0;
                     const unsigned long long need = (unsigned long long)(b - kPipeLag + 1);
@@ -840,6 +843,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap) P.trace[b * kTraceCols + 13] = (uint64_t)pc->s_ex;
             if (lane == 0) { ex_rows += scr ? pc->s_ex : Rvalid; scan_rows += Rvalid; }
             // ---- arrive (the merge waves of workgroups 1 .. B wait for all G) ----
+            jitter_at(P.jitter, b, 2);
             const int slot = (int)((nact - 1) % 4);
             if (lane == 0) {
                 if (g == 0) trace_at(P, b, 5);
@@ -1107,6 +1111,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         // (commit(b - 2) usually ends well before the batch's last arrival): off the merge -> commit path
         if (P.inh && b >= 2) {
             if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit)) return;
+            jitter_at(P.jitter, b, 3);
             for (int m = g; m < P.B; m += kMS * P.M)
                 if (p0 + m < NP) inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid);
         }
@@ -1184,6 +1189,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
 #endif
                 if (mtid < 64) rank_merge_msgs<K>(s_all, RR, ma.out_rec + (size_t)m * K, ma.out_fc + m);
             }
+            jitter_at(P.jitter, b, 4 + m);
             drain_stores();
             sync();  // every merge wave's stores drained before the count; LDS free for the next pod
 #if KSCHED_XCHG_DEBUG
@@ -1221,6 +1227,8 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
     __builtin_amdgcn_s_setprio(3);
     PersistLocal &loc = *reinterpret_cast<PersistLocal *>(smem);
     char *cs = smem + commit_loc_bytes();
+    uint32_t *canary = reinterpret_cast<uint32_t *>(cs - kCanaryBytes);
+    if (threadIdx.x < kCanaryBytes / 4) canary[threadIdx.x] = 0xA5A5A5A5u ^ threadIdx.x;
     __shared__ int s_stop;
     __shared__ HandoffRes s_ho;
     __shared__ int s_hr;
@@ -1249,7 +1257,14 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         const int64_t pm = b >= 4 ? loc.plan[(b - 1) % kPlanRing] : b >= 1 ? (int64_t)ld_coh(&ctl->plan[(b - 1) % kPlanRing]) : -1;
         const bool act = p0 >= 0 && p0 < P.pods.p;
         nact += ((b >= 1 && pm >= 0 && pm < P.pods.p) ? 1 : 0) + (act ? 1 : 0);
-        if (b < 2 && threadIdx.x == 0) loc.plan[b % kPlanRing] = p0;
+        jitter_at(P.jitter, b, 100);  // the commit workgroup's loop top
+        if (b < 2) {
+            // the first two plans reach the LDS copy here; every wave reads it (commit_spc_batch) only after this
+            // barrier -- without it a wave could read the copy before thread 0 wrote it: an LDS word left by an
+            // earlier kernel (round 5: a fresh engine then took the idle path on some waves only)
+            if (threadIdx.x == 0) loc.plan[b % kPlanRing] = p0;
+            __syncthreads();
+        }
         if (!act && ++idle > kPlanRing) {
             // pods remain but nothing is planned: a truncation re-plans within kPipeLag batches, so this is a
             // protocol error -- stop everyone instead of spinning
@@ -1385,6 +1400,11 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
             return;
         }
         __syncthreads();
+        if (threadIdx.x < kCanaryBytes / 4 && canary[threadIdx.x] != (0xA5A5A5A5u ^ threadIdx.x)) {
+            // an LDS write below the commit's arrays: report which word, once
+            if (atomicCAS(P.err, 0, 15) == 0 && P.prog)
+                P.prog[kProgWords * cslot + 2] = (uint64_t)b << 32 | (uint64_t)threadIdx.x << 16 | (canary[threadIdx.x] & 0xffffu);
+        }
         if (threadIdx.x == 0) {
             trace_at(P, b, 4);
             prog_at(P, cslot, b, kProgCommitted, 0);
@@ -1408,8 +1428,14 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
     for (int i = 1; i < kMaxLocalRanks; ++i) r += (i < L.R && (int)blockIdx.x >= L.base[i]) ? 1 : 0;
     const PersistArgs &P = L.P[r];
     const int blk = (int)blockIdx.x - L.base[r];
-    if (P.poison_lds) {  // diagnostics: any LDS read before its write then sees 0xff bytes, not a predecessor's data
-        for (int i = (int)threadIdx.x; i < P.poison_lds / 4; i += kPipeThreads) reinterpret_cast<uint32_t *>(smem)[i] = ~0u;
+    if (P.poison_lds) {  // diagnostics: any LDS read before its write then sees the fill, not a predecessor's data
+        const int role = blk < kCommitWGs ? 1 : (blk < kCommitWGs + P.G ? 2 : 4);
+        // role bit 8: a distinct pattern per role (the fill ^ role * 0x01010101), so a value read before its write
+        // names the role whose LDS it came from
+        const uint32_t fill = (P.lds_fill_role & 8) ? P.lds_fill ^ ((uint32_t)role * 0x01010101u) : P.lds_fill;
+        if (P.lds_fill_role & role)
+            for (int i = (int)threadIdx.x; i < P.poison_lds / 4; i += kPipeThreads)
+                if (4 * i >= P.lds_fill_lo && 4 * i < P.lds_fill_hi) reinterpret_cast<uint32_t *>(smem)[i] = fill;
         __syncthreads();
     }
     if (blk < kCommitWGs) {

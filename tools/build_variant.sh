@@ -7,7 +7,7 @@ name=$1; defs=$2
 cd "$(dirname "$0")/../k8s-scheduler_amd"
 make -s -j8 >/dev/null
 mkdir -p build_$name
-HIPFLAGS="-O3 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -std=c++17 -I../include -Icsrc -Wall -Wno-unused-result -Wno-unused-value --offload-arch=gfx950"
+HIPFLAGS="-O3 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fno-strict-aliasing -fPIC -std=c++17 -I../include -Icsrc -Wall -Wno-unused-result -Wno-unused-value --offload-arch=gfx950"
 for p in 0 1 2; do
   /opt/rocm/bin/hipcc $HIPFLAGS $defs -DKSCHED_PIPE_PART=$p -c csrc/ksched_pipe.hip -o build_$name/ksched_pipe$p.o &
 done
