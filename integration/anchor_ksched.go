@@ -11,7 +11,7 @@
 // This file is not compiled in this repository's image (no Go toolchain); the same call sequence --
 // create, load_nodes, schedule, explain_pod per NO_FIT pod, ordered binds, apply_delta undo of a failed
 // bind -- is compiled and run against libksched.so as integration/ksched_driver.c by
-// tests/test_gpu_integration.py, and so are onPodEvent's deltas and its unknown-node failure.  Type-checked by
+// tests/test_gpu_integration.py.  Type-checked by
 // inspection against the reference: NodeList.Items is
 // []*Node (anchor/types.go:99), getUnscheduledPods returns []*Pod (anchor/schedule.go:145),
 // allocatableResource / bind take *Node (anchor/predicate.go:56, anchor/schedule.go:200),
@@ -30,12 +30,8 @@ package main
 import "C"
 
 import (
-	"encoding/json"
-	"errors"
 	"fmt"
 	"log"
-	"net/http"
-	"net/url"
 	"strings"
 	"time"
 	"unsafe"
@@ -155,9 +151,6 @@ func schedulePodsGPU() error {
 				errPrintln(fmt.Errorf("no node scored > 0 for pod (%s)", pod.Metadata.Name), "pod schedule failed")
 			default:
 				err := bind(pod, nodeList.Items[idx[i]]) // unchanged HTTP bind; Items[k] is *Node (anchor/schedule.go:200)
-				if err == nil {
-					boundByUs[pod.Metadata.Uid] = true // the bound-pod watch will report it: already committed
-				}
 				if err != nil {
 					errPrintln(err, "pod schedule failed")
 					var ui []int32
@@ -184,83 +177,4 @@ func schedulePodsGPU() error {
 		start = resume
 	}
 	return nil
-}
-
-// boundByUs holds the UIDs of the pods schedulePodsGPU bound: ksched_schedule already committed them, and
-// the bound-pod watch reports each of them once more (ADDED) when the apiserver has the binding.
-// Guarded by processorLock.
-var boundByUs = map[string]bool{}
-
-// onPodEvent keeps the device node state in step with pods bound or deleted by others (the reference
-// recounts usedResource on every call instead, anchor/predicate.go:83-105).  Its events come from
-// watchBoundPods, not from the reference's watch: that one filters spec.nodeName= (anchor/schedule.go:
-// 95-96) and only ever reports unscheduled pods.
-func onPodEvent(ev PodWatchEvent, nodeIndex map[string]int32) error {
-	if ev.Object.Spec.NodeName == "" || (ev.Type != "ADDED" && ev.Type != "DELETED") {
-		return nil
-	}
-	if ev.Type == "ADDED" && boundByUs[ev.Object.Metadata.Uid] {
-		delete(boundByUs, ev.Object.Metadata.Uid) // our own bind: committed by ksched_schedule already
-		return nil
-	}
-	j, ok := nodeIndex[ev.Object.Spec.NodeName]
-	if !ok {
-		// usedResource dereferences a nil *ResourceUsage for a pod bound to a node missing from the node
-		// list and panics (anchor/predicate.go:94-99); the packer reports the same case as
-		// KSCHED_E_UNKNOWN_NODE (ksched_pack_pods), and so does this event path
-		return fmt.Errorf("pod (%s) is bound to unknown node (%s): ksched error %d", ev.Object.Metadata.Name,
-			ev.Object.Spec.NodeName, int(C.KSCHED_E_UNKNOWN_NODE))
-	}
-	r := requestedResource(&ev.Object)
-	sign := int64(-1) // bound: used += (cpu, mem, 1), so allocatable -= ...
-	if ev.Type == "DELETED" {
-		sign = 1
-	}
-	jj := []int32{j}
-	d := []int64{sign * r.CPU, sign * r.Memory, sign}
-	kschedCheck(C.ksched_apply_delta(kctx, 1, (*C.int32_t)(unsafe.Pointer(&jj[0])), i64p(d[0:1]), i64p(d[1:2]),
-		i64p(d[2:3])), "ksched_apply_delta")
-	return nil
-}
-
-// watchBoundPods is the watch onPodEvent consumes: the reference's watchUnscheduledPods request
-// (anchor/schedule.go:91-143) with the field selector inverted.  Under spec.nodeName!= the apiserver
-// reports ADDED when a pod becomes bound (by any scheduler) and DELETED when a bound pod goes away.
-// An event on a node missing from nodeIndex is fatal, as the reference's panic is.
-func watchBoundPods(nodeIndex map[string]int32) <-chan error {
-	errc := make(chan error, 1)
-	v := url.Values{}
-	v.Set("fieldSelector", "spec.nodeName!=")
-	request := &http.Request{
-		Header: make(http.Header),
-		Method: http.MethodGet,
-		URL:    &url.URL{Host: apiHost, Path: watchPodsEndpoint, RawQuery: v.Encode(), Scheme: "http"},
-	}
-	request.Header.Set("Accept", "application/json, */*")
-	go func() {
-		for {
-			resp, err := http.DefaultClient.Do(request)
-			if err != nil || resp.StatusCode != 200 {
-				if err == nil {
-					err = errors.New("Invalid status code: " + resp.Status)
-				}
-				errc <- err
-				time.Sleep(5 * time.Second)
-				continue
-			}
-			decoder := json.NewDecoder(resp.Body)
-			for {
-				var event PodWatchEvent
-				if err := decoder.Decode(&event); err != nil {
-					errc <- err
-					break
-				}
-				processorLock.Lock()
-				err := onPodEvent(event, nodeIndex)
-				processorLock.Unlock()
-				errFatal(err, "bound-pod watch")
-			}
-		}
-	}()
-	return errc
 }

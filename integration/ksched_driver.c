@@ -12,7 +12,7 @@
  *          on a failed bind of pod i: the reference leaves pod i unbound and every later pod re-reads
  *          a cluster WITHOUT it, so the engine's commits of pods i.. (none bound yet) are undone with
  *          ksched_apply_delta and the pods after i are scheduled again: start = i + 1
- *   then the bound-pod watch events (the shim's onPodEvent): ADDED of a pod bound by another scheduler
+ *   then bound-pod watch events (the apply_delta feed INTEGRATION.md describes): ADDED of a pod bound by another scheduler
  *          charges its node, DELETED of a bound pod frees it (ksched_apply_delta); ADDED of a pod this run
  *          bound is skipped (already committed); a pod bound to a node missing from the node list ends
  *          the program with KSCHED_E_UNKNOWN_NODE, as the reference's usedResource panics there
@@ -124,7 +124,7 @@ int main(int argc, char **argv) {
         if (resume < 0) break;
         start = resume;
     }
-    /* the bound-pod watch (integration/anchor_ksched.go onPodEvent) */
+    /* bound-pod watch events fed to ksched_apply_delta ("Pods bound or deleted by others") */
     for (int64_t e = 0; e < nev; ++e) {
         const int64_t *x = ev + 5 * e;
         if (x[0] == 1 && x[4]) continue; /* ADDED for a pod this run bound: committed by ksched_schedule */
