@@ -722,6 +722,16 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     int32_t my_g = -2, my_q = -1, my_s = -1, my_h = kSpcInvalid;
     int nT = nin, done = nb, W = 64;
     int nresc = 0;  // wave 0: rescues of this batch
+    // wave 0: quarter rescues this batch may spend -- the persistent commit's bucket refills by rescue_rate per
+    // batch of this workgroup up to 4 * rescue_max, so exhausted lists are rescued where they are rare and
+    // truncate early where they cluster (the rescues of a batch that truncates anyway are wasted)
+    // and a batch may spend rescue_max of them while the bucket is at least half full, rescue_low below that
+    int rcredit = 0, rmax = 0;
+    if constexpr (COH) {
+        const int c = A.loc->rescue_credit + A.rescue_rate;
+        rcredit = c < 4 * A.rescue_cap ? c : 4 * A.rescue_cap;
+        rmax = rcredit >= 2 * A.rescue_cap ? A.rescue_max : A.rescue_low;
+    }
     int64_t placed = 0, nrounds = 0, nfail = 0, niters = 0, nseq = 0;
     if (wave == 0) {
         int64_t ds2 = 0;
@@ -1060,7 +1070,26 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                 RescueOut ro{};
                 if constexpr (COH) {
                     // the persistent commit (one rank) rescues an exhausted list instead of truncating the batch
-                    if (kf == 3 && A.rescue && nresc < A.rescue_max &&
+                    bool afford = kf == 3 && A.rescue && nresc < rmax && 4 * (nresc + 1) <= rcredit;
+                    if (afford && A.rescue_look) {
+                        // look ahead: the later pods of the batch whose cut list is exhausted already (every entry a
+                        // touched node).  When they would overrun the credit the batch truncates anyway -- a rescue
+                        // before that truncation is wasted -- so it truncates here
+                        bool risk = false;
+                        if (lane > f && lane < nb && cut) {
+                            risk = true;
+#pragma unroll
+                            for (int q = 0; q < K; ++q) {
+                                if (q < cv) {
+                                    const int pos = m.HP[q * 64 + lane];
+                                    risk = risk && ((m.tkc[pos >> 5] >> (pos & 31)) & 1u);
+                                }
+                            }
+                        }
+                        const int n = nresc + 1 + __popcll(__ballot(risk));
+                        afford = n <= rmax && 4 * n <= rcredit;
+                    }
+                    if (afford &&
                         commit_rescue(A, f, rl64(rc, f), rl64(rm, f), rl64(rp, f), (uint64_t)rl64((int64_t)sel, f),
                                       m.ti, nT, &ro)) {
                         ++nresc;
@@ -1304,6 +1333,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             __hip_atomic_fetch_add(st + 2, (unsigned long long)placed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (nresc) __hip_atomic_fetch_add(st + 4, (unsigned long long)nresc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (threadIdx.x == 0) A.loc->rescue_credit = rcredit - 4 * nresc;
     }
     return 1;
 }

@@ -209,9 +209,17 @@ struct ksched_ctx {
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
         uint32_t jitter = 0;     // KSCHED_JITTER=<seed>: random delays at the persistent pipeline's protocol points
         bool touch_screen = true;  // KSCHED_NO_TOUCH_SCREEN=1: the commit keys every touched node exactly
-        int rescue_max = 4;      // KSCHED_RESCUE_MAX: rescues per batch (0: exhausted lists always truncate); a
-                                 // rescue costs ~20 us of the commit's loop, a truncation ~2 voided batches
-                                 // (the budget table)
+        // the rescue policy (the rescue table).  A rescue costs ~20 us of the commit's loop,
+        // a truncation ~2 voided batches, so rescues pay where exhausted lists are rare and lose where they cluster
+        // (the rescues of a batch that truncates anyway are wasted).  Each commit workgroup keeps a bucket of
+        // credit: rescue_rate quarter rescues per batch of its own, at most rescue_cap rescues; a batch spends at
+        // most rescue_max while the bucket is at least half full and rescue_low below that
+        int rescue_max = 4;      // KSCHED_RESCUE_MAX (0: exhausted lists always truncate)
+        int rescue_rate = 4;     // KSCHED_RESCUE_RATE, quarter rescues per batch of the workgroup
+        int rescue_cap = 16;     // KSCHED_RESCUE_CAP
+        int rescue_low = 2;      // KSCHED_RESCUE_LOW
+        int rescue_look = 0;     // KSCHED_RESCUE_LOOK=1: also truncate when the batch's other exhausted lists would
+                                 // overrun the allowance (helps a fixed budget, loses with the bucket)
         int64_t persist_timeout_ms = 10000, exchange_timeout_ms = 2000;
     } diag;
 };
@@ -867,6 +875,10 @@ int enqueue_persistent(ksched_ctx *c) {
     // results through the rings (ksched_commit.h rescue_rank_fold)
     a.rescue = c->diag.rescue_max <= 0 ? nullptr : reinterpret_cast<char *>(a.prog) + prog_b;
     a.rescue_max = c->diag.rescue_max;
+    a.rescue_rate = c->diag.rescue_rate;
+    a.rescue_look = c->diag.rescue_look;
+    a.rescue_cap = c->diag.rescue_cap;
+    a.rescue_low = c->diag.rescue_low;
     a.touch_screen = c->diag.touch_screen ? 1 : 0;
     if (c->diag.jitter) a.jitter = c->diag.jitter * 2654435761u + (uint32_t)(++c->jitter_calls) * 40503u + 1u;
     a.inh = reinterpret_cast<char *>(a.prog) + prog_b + resc_b;
@@ -1096,6 +1108,10 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
     c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
+    c->diag.rescue_rate = env_int("KSCHED_RESCUE_RATE", 4);
+    c->diag.rescue_look = env_int("KSCHED_RESCUE_LOOK", 0);
+    c->diag.rescue_cap = env_int("KSCHED_RESCUE_CAP", 16);
+    c->diag.rescue_low = env_int("KSCHED_RESCUE_LOW", 2);
     c->diag.touch_screen = env_int("KSCHED_NO_TOUCH_SCREEN", 0) == 0;
     c->diag.jitter = (uint32_t)env_int("KSCHED_JITTER", 0);
     c->diag.persist_timeout_ms = env_int("KSCHED_PERSIST_TIMEOUT_MS", 10000);

@@ -257,6 +257,7 @@ struct PersistLocal {
     int32_t xcount;   // entries of the previous batch's export
     int32_t xcount2;  // entries of the export of the batch before it (both are inherited: lag kPipeLag)
     int64_t rseq;     // rescue requests issued this call
+    int32_t rescue_credit;  // the rescue bucket, in quarter rescues (CommitArgs::rescue_rate)
 };
 
 struct PersistArgs;
@@ -281,6 +282,11 @@ struct CommitArgs {
     char *rescue;           // persistent pipeline: the rescue request / results (else null: truncate)
     int32_t rescue_n;       // merger slots serving a rescue (= B)
     int32_t rescue_max;     // rescues per batch; the next exhausted list truncates the batch
+    int32_t rescue_cap;     // persistent: the rescue bucket's capacity, in rescues
+    int32_t rescue_low;     // persistent: rescues per batch while the bucket is below half full
+    int32_t rescue_look;    // persistent: skip a rescue when the batch's exhausted lists already overrun the credit
+    int32_t rescue_rate;    // persistent: the bucket's refill per batch of this workgroup, in quarter rescues (a batch
+                            // spends at most min(rescue_max, credit) rescues; rate >= 4 * rescue_max: a fixed budget)
     int32_t touch_screen;   // persistent commit: the touched-node screen on (KSCHED_NO_TOUCH_SCREEN=1 turns it off)
     const char *inh;        // persistent commit: the mergers' keys of the older export (inherit_x2_keys), else null
     int64_t timeout_ticks;  // bound of the rescue wait
@@ -490,6 +496,10 @@ struct PersistArgs {
     int32_t lds_fill_lo, lds_fill_hi;  // byte range filled (KSCHED_LDS_LO / KSCHED_LDS_HI)
     uint32_t jitter;        // diagnostics (KSCHED_JITTER): seed of the random delays at the protocol points, 0 = off
     int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
+    int32_t rescue_cap;     // the rescue bucket's capacity in rescues (KSCHED_RESCUE_CAP, default rescue_max)
+    int32_t rescue_low;     // rescues per batch while the bucket is below half full (KSCHED_RESCUE_LOW)
+    int32_t rescue_look;    // KSCHED_RESCUE_LOOK (default 1): the commit's look-ahead over the batch's exhausted lists
+    int32_t rescue_rate;    // the commit workgroup's rescue bucket refill per batch, quarter rescues (KSCHED_RESCUE_RATE)
     int32_t touch_screen;   // the commit's touched-node screen (KSCHED_NO_TOUCH_SCREEN=1: every key exact)
     // the merger slots' keys of their pod against the entries of export(b - 2), which commit(b) inherits:
     // [4 batches][B] summaries {sum of predicate deltas, best key, best idx | entry << 32, -} then [4][B][64] keys

@@ -1240,6 +1240,7 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         loc.xcount = 0;
         loc.xcount2 = 0;
         loc.rseq = 0;
+        loc.rescue_credit = 4 * P.rescue_cap;
     }
     __syncthreads();
     const int64_t cursor0 = loc.cursor;
@@ -1388,6 +1389,10 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
         ca.dbg_act = nact - 1;
         ca.rescue_n = P.B;
         ca.rescue_max = P.rescue_max;
+        ca.rescue_rate = P.rescue_rate;
+        ca.rescue_look = P.rescue_look;
+        ca.rescue_cap = P.rescue_cap;
+        ca.rescue_low = P.rescue_low;
         ca.touch_screen = P.touch_screen;
         ca.inh = P.inh;
         ca.timeout_ticks = P.timeout_ticks;

@@ -3,6 +3,8 @@
 
   python tools/sweep.py c3:exact c3:batched:16:128 c4:batched:16:256 ...
 spec = config[:mode[:topk[:batch[:pods[:nodes]]]]]
+An argument @NAME=V[,NAME=V...] sets engine environment switches (read at engine creation) for the specs after it,
+e.g. @KSCHED_RESCUE_MAX=4,KSCHED_RESCUE_RATE=4; each line names them in "env".
 """
 import json
 import os
@@ -46,12 +48,20 @@ def run(spec, reps=2):
                truncations=st["truncations"], rescues=st.get("rescues"), pipeline=st.get("pipeline"),
                device_ms=st["device_ms"],
                fam_avg_ms=[st["kernel_ms"][f] / max(st["kernel_launches"][f], 1) for f in range(4)],
-               fam_timed=st["kernel_launches"])
+               fam_timed=st["kernel_launches"], env=ENV_TAG)
     print(json.dumps(out), flush=True)
 
 
+ENV_TAG = ""
+
 if __name__ == "__main__":
     for s in sys.argv[1:]:
+        if s.startswith("@"):
+            ENV_TAG = s[1:]
+            for kv in ENV_TAG.split(","):
+                k, v = kv.split("=", 1)
+                os.environ[k] = v
+            continue
         try:
             run(s)
         except Exception as ex:
