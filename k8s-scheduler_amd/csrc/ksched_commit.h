@@ -23,6 +23,9 @@
 
 #include <hip/hip_runtime.h>
 
+#ifndef KSCHED_RESCAN_UNROLL
+#define KSCHED_RESCAN_UNROLL 1  // the sequential path's touched-slot rescan with four loads in flight
+#endif
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tests/diag/xchg_ring_experiment.py (a separate build)
 #endif
@@ -1190,12 +1193,41 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                         rbk = up ? kv : rbk; rbi = up ? wi : rbi; rbs = up ? s : rbs;
                         if (__ballot(rescan)) {
                             if (rescan) {
+#if KSCHED_RESCAN_UNROLL
+                                // four slots' loads in flight, two running maxima (better() is a total order on
+                                // distinct nodes, so the fold order does not change the result)
+                                double k0 = -__builtin_inf(), k1 = -__builtin_inf();
+                                int32_t i0 = kNoIdx, i1 = kNoIdx;
+                                int s0 = -1, s1 = -1;
+                                int t = 0;
+                                for (; t + 4 <= nT; t += 4) {
+                                    double v[4];
+                                    int32_t x[4];
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u) { v[u] = Srow[t + u]; x[u] = m.ti[t + u]; }
+#pragma unroll
+                                    for (int u = 0; u < 4; u += 2) {
+                                        if (v[u] != -__builtin_inf() && better(v[u], x[u], k0, i0)) { k0 = v[u]; i0 = x[u]; s0 = t + u; }
+                                        if (v[u + 1] != -__builtin_inf() && better(v[u + 1], x[u + 1], k1, i1)) {
+                                            k1 = v[u + 1]; i1 = x[u + 1]; s1 = t + u + 1;
+                                        }
+                                    }
+                                }
+                                for (; t < nT; ++t) {
+                                    const double v = Srow[t];
+                                    const int32_t x = m.ti[t];
+                                    if (v != -__builtin_inf() && better(v, x, k0, i0)) { k0 = v; i0 = x; s0 = t; }
+                                }
+                                if (k1 != -__builtin_inf() && better(k1, i1, k0, i0)) { k0 = k1; i0 = i1; s0 = s1; }
+                                rbk = k0; rbi = i0; rbs = s0;
+#else
                                 rbk = -__builtin_inf(); rbi = kNoIdx; rbs = -1;
                                 for (int t = 0; t < nT; ++t) {
                                     const double v = Srow[t];
                                     const int32_t x = m.ti[t];
                                     if (v != -__builtin_inf() && better(v, x, rbk, rbi)) { rbk = v; rbi = x; rbs = t; }
                                 }
+#endif
                             }
                         }
                     }
