@@ -316,3 +316,30 @@ def test_persistent_pipeline_parity(gpu_available, oracle_mod, name, nn, pp):
         got = run_engine(cl, MODE_BATCHED, **kw)
         assert_same(got, want, f"{name}/{kw}")
         assert got[4]["pipeline"] == "persistent", got[4]
+
+
+@pytest.mark.parametrize("policy", ["none", "fixed4", "bucket", "scarce", "look"])
+def test_rescue_policies_same_results(gpu_available, oracle_mod, monkeypatch, policy):
+    """The rescue policy (KSCHED_RESCUE_*, DESIGN 4.1: truncate always, a fixed budget per batch, the default
+    credit bucket, a scarce bucket, the look-ahead) decides only whether an exhausted candidate list is rescued
+    or truncates its batch -- never a result: every policy is bit-exact against the oracle on a high-conflict
+    cluster with short lists, and the counters show which path ran."""
+    from ksched import MODE_BATCHED, cluster
+    env = {"none": dict(KSCHED_RESCUE_MAX="0"),
+           "fixed4": dict(KSCHED_RESCUE_MAX="4", KSCHED_RESCUE_RATE="16", KSCHED_RESCUE_CAP="4", KSCHED_RESCUE_LOW="4"),
+           "bucket": {},
+           "scarce": dict(KSCHED_RESCUE_MAX="2", KSCHED_RESCUE_RATE="1", KSCHED_RESCUE_CAP="2", KSCHED_RESCUE_LOW="1"),
+           "look": dict(KSCHED_RESCUE_LOOK="1")}[policy]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cl = cluster.make_cluster("c5hc", n_nodes=20000, n_pods=3000)
+    want = oracle_mod.schedule(cl, nthreads=8)
+    got = run_engine(cl, MODE_BATCHED, topk=4, batch=64, chunk_topk=4)
+    assert_same(got, want, f"c5hc/{policy}")
+    st = got[4]
+    print(f"{policy}: batches {st['batches']} truncations {st['truncations']} rescues {st['rescues']}")
+    assert st["pipeline"] == "persistent", st
+    if policy == "none":
+        assert st["rescues"] == 0 and st["truncations"] > 0, st
+    else:
+        assert st["rescues"] > 0, st
