@@ -47,6 +47,9 @@ constexpr int kPU = 4;                 // rows per score step (independent key c
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0
 #endif
+#ifndef KSCHED_REC_PKRTZ
+#define KSCHED_REC_PKRTZ 1  // pass 1's two records per v_cvt_pkrtz_f16_f32
+#endif
 #ifndef KSCHED_SCREEN_PU
 #define KSCHED_SCREEN_PU 4
 #endif
@@ -558,6 +561,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                     uint32_t xs[kSPU];
                     uint32_t hh[kSPU];
                     uint32_t ambm = 0;  // rows of this group with an ambiguous fraction for this lane's pod
+#if KSCHED_REC_PKRTZ
+                    float vv[kSPU];
+                    bool nrm[kSPU];
+#endif
 #pragma unroll
                     for (int u = 0; u < kSPU; ++u) {
                         const int r = r0 + u * kSW;
@@ -573,14 +580,30 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         xs[u] = (valid && active && el && lo_ok && !amb) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
                         // the pair's upper bound (screen_rec): 0 (always needed) when ambiguous, 0xffff (never
                         // needed) without a key
+#if KSCHED_REC_PKRTZ
+                        vv[u] = v;
+                        nrm[u] = !amb && el;
+                        hh[u] = amb ? 0u : 0xffffu;
+#else
                         hh[u] = amb ? 0u : (el ? screen_rec(v) : 0xffffu);
+#endif
                         ambm |= (valid && amb) ? 1u << u : 0u;
                     }
                     // the records of rows k, k + 1 (k = (r0 - wave) / kSW + u, u even) in one store; a pair's second
                     // row past the wave's last is never read
 #pragma unroll
-                    for (int u = 0; u < kSPU; u += 2)
-                        if (r0 + u * kSW < Rv) hw[(size_t)(((r0 - wave) / kSW + u) / 2) * 64] = hh[u] | (hh[u + 1] << 16);
+                    for (int u = 0; u < kSPU; u += 2) {
+#if KSCHED_REC_PKRTZ
+                        // both rows' screen_rec in one conversion: round toward zero IS its round-down for w >= 0
+                        const uint32_t rec = __builtin_bit_cast(
+                            uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_fmaxf(10.0f - vv[u], 0.0f),
+                                                                 __builtin_fmaxf(10.0f - vv[u + 1], 0.0f)));
+                        const uint32_t w2 = (nrm[u] ? (rec & 0xffffu) : hh[u]) | ((nrm[u + 1] ? (rec >> 16) : hh[u + 1]) << 16);
+#else
+                        const uint32_t w2 = hh[u] | (hh[u + 1] << 16);
+#endif
+                        if (r0 + u * kSW < Rv) hw[(size_t)(((r0 - wave) / kSW + u) / 2) * 64] = w2;
+                    }
                     if (__ballot(ambm != 0)) {  // wave-uniform, rare: queue the rows with an ambiguous pair
 #pragma unroll
                         for (int u = 0; u < kSPU; ++u) {
