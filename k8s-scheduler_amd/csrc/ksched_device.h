@@ -288,25 +288,39 @@ __device__ __forceinline__ float screen_q(float c, float m, float p, bool okc, b
     return v;
 }
 
-// The screened scan's per-pair record (pass 1 -> pass 2): a 16-bit upper bound of a screen value v (<= 10; NaN
-// allowed), 10 - value(h) >= v - 2^-21, as the f16 bit pattern h of w = RN(10 - v) rounded DOWN (RN, then one
-// ulp less when that rounded up; NaN -> w = 0, always needed).  w >= 0, so patterns order as values and pass 2
-// compares them as integers against screen_rec_threshold; f16's relative precision keeps the bound tight where
-// the keys crowd (v near 10, small w).  0xffff: no key (above every threshold).
-__device__ __forceinline__ uint32_t screen_rec(float v) {
-    const float w = __builtin_fmaxf(10.0f - v, 0.0f);  // NaN -> 0 (maxNum)
+// The screened scan's per-pair record (pass 1 -> pass 2): a 16-bit upper bound of a screen value v (NaN allowed),
+// in two forms by the pair's screen form (screen_q's rf):
+//   resource-fitting (polynomial, v <= 10): the f16 bit pattern h of w = RN(10 - v) rounded DOWN (round toward
+//     zero: v_cvt_pkrtz_f16_f32 of two rows at once), so 10 - value(h) >= v - 2^-21; bit 15 clear;
+//   non-fitting (v <= (5/3) * 2 < kNfBase): the same of w = RN(kNfBase - v), with bit 15 set -- f16's relative
+//     precision is then fine near the non-fitting keys (~3.3: late in c4 most pods fit nowhere and rank only
+//     these), where 10 - v was coarse (ulp 2^-8 at w ~ 6.7).
+// NaN -> w = 0 (maxNum): always needed.  0 = always needed, 0xffff = no key (a non-fitting NaN pattern, above every
+// threshold).  Pass 2 compares the 15 low bits as integers against the form's threshold (screen_rec_threshold).
+constexpr float kNfBase = 3.375f;  // > every non-fitting screen value (<= (5/3) * 2 + rounding)
+__device__ __forceinline__ uint32_t screen_rec_w(float w) {  // f16 pattern of w >= 0 rounded down
     const _Float16 h = (_Float16)w;
     const uint32_t hb = (uint32_t)__builtin_bit_cast(uint16_t, h);
     return hb - ((float)h > w ? 1u : 0u);
 }
-// The largest record (+ one) a pod needs with bound L (shifted by +1, 0 = none): 10 - value(h) + 2^-20 + 1 + eps
-// >= L  <=>  value(h) <= T = 11 + eps + 2^-20 - L; -1 when T < 0.  RN to f16 of T (as f32), plus one pattern:
-// a superset of the exact test (tests/test_screen_bound.py)
-__device__ __forceinline__ int screen_rec_threshold(float L) {
-    const double T = 11.0 + (double)kScreenEps + 0x1p-20 - (double)L;
+__device__ __forceinline__ uint32_t screen_rec(float v) { return screen_rec_w(__builtin_fmaxf(10.0f - v, 0.0f)); }
+__device__ __forceinline__ uint32_t screen_rec_nf(float v) {
+    return 0x8000u | screen_rec_w(__builtin_fmaxf(kNfBase - v, 0.0f));
+}
+// The largest record (+ one) a pod needs with bound L (shifted by +1, 0 = none): base - value(h) + 2^-20 + 1 + eps
+// >= L  <=>  value(h) <= T = base + 1 + eps + 2^-20 - L; -1 when T < 0.  RN to f16 of T (as f32), plus one pattern:
+// a superset of the exact test (tests/test_screen_bound.py).  base = 10 (resource-fitting records) or kNfBase.
+__device__ __forceinline__ int screen_rec_threshold_at(double base, float L) {
+    const double T = base + 1.0 + (double)kScreenEps + 0x1p-20 - (double)L;
     if (!(T >= 0.0)) return -1;
     const _Float16 h = (_Float16)(float)T;
     return (int)__builtin_bit_cast(uint16_t, h) + 1;
+}
+__device__ __forceinline__ int screen_rec_threshold(float L) { return screen_rec_threshold_at(10.0, L); }
+__device__ __forceinline__ int screen_rec_threshold_nf(float L) { return screen_rec_threshold_at((double)kNfBase, L); }
+// pass 2's test of one record against the pod's two thresholds (-1, -1: an inactive lane)
+__device__ __forceinline__ bool screen_rec_needed(uint32_t h, int tq, int tqn) {
+    return (h & 0x8000u) ? (int)(h & 0x7fffu) <= tqn : (int)h <= tq;
 }
 
 // The screen of one pair.  ok* = (a_k >= r_k) per resource (exact int64 compares).  Returns the f32 value

@@ -203,8 +203,10 @@ struct ksched_ctx {
     struct {
         bool trace = false, commit_stamps = false, merge_stamps = false, debug = false;
         bool no_screen = false;  // KSCHED_NO_SCREEN: the exact scan everywhere (A/B of the screened scan)
+        bool no_pairs = false;   // KSCHED_NO_PAIRS: the screened scan's exact phase by rows (A/B of the pair lists)
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
         int xchg_diag = 0;       // KSCHED_XCHG_DIAG (section 6.1's experiment): 1 ring zeroed by hipMemsetAsync, 2 local tags from 1
+        int64_t epoch_base = 0;  // KSCHED_XCHG_EPOCH_BASE (tests): a setup's granule tags start at least here (near 2^15: wrap)
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
         uint32_t jitter = 0;     // KSCHED_JITTER=<seed>: random delays at the persistent pipeline's protocol points
@@ -455,6 +457,24 @@ int rx_map_peer(ksched_ctx *c, int r, const uint8_t *handle) {
     return KSCHED_OK;
 }
 
+// Before every call's rank barrier each rank zeroes its own ring's message and rescue areas (not the barrier
+// granules the barrier itself uses): granule tags keep 15 bits (gran_tag), so a region a call does not rewrite --
+// the rescue area when no rescue happens, the message slots of a call with fewer than four active batches -- could
+// otherwise hold, calls later, a granule whose tag matches a wait modulo 2^15.  A peer writes into this
+// ring only after it has seen this rank at the barrier, which this rank reaches after the zeroing kernel finished
+// (stream order), so no granule of the call is lost.  Within a call a region is rewritten every 4 active batches
+// (messages) or every 2 rescues, and both are zeroed again by the next call.
+int rx_zero_regions(ksched_ctx *c) {
+    const int R = c->o.nranks;
+    const size_t stride = xchg_stride_bytes(c->K);
+    const size_t msg = (size_t)4 * R * c->B * stride;
+    const size_t resc = xchg_rescue_off(R, c->B, stride);
+    if (!c->d_rx || c->rx_bytes < xchg_ring_bytes(R, c->B, c->K)) return fail(c, KSCHED_E_STATE, "exchange ring missing");
+    HIPCHK(c, launch_zero_sys(c->d_rx, msg, c->stream));
+    HIPCHK(c, launch_zero_sys(static_cast<char *>(c->d_rx) + resc, 2 * (size_t)R * kXchgRescueRec, c->stream));
+    return KSCHED_OK;
+}
+
 // fast53 for this call: every |alloc| + sum of |requests| < 2^52, on every rank.
 int decide_fast53(ksched_ctx *c) {
     int flag = sat_add(c->max_abs_alloc, c->sum_abs_req) < (1ull << 52) ? 1 : 0;
@@ -465,6 +485,8 @@ int decide_fast53(ksched_ctx *c) {
     } else if (c->xchg_run && c->lg) {
         ksched_lgroup *g = c->lg.get();
         int mn = flag;
+        if (int rc = rx_zero_regions(c); rc != KSCHED_OK) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // finished before any rank of the group can launch
         if (!lg_meet(g, [&] { g->acc = g->arrived == 0 ? flag : std::min(g->acc, flag); }, [&] { g->result = g->acc; }))
             return fail(c, KSCHED_E_DEVICE, "local rank group: a peer never called run");
         mn = g->result;
@@ -476,6 +498,7 @@ int decide_fast53(ksched_ctx *c) {
         a.err = c->d_err;
         a.timeout_ticks = c->diag.persist_timeout_ms * 100000;
         int32_t mn = -1;
+        if (int rc = rx_zero_regions(c); rc != KSCHED_OK) return rc;  // stream-ordered before the barrier
         HIPCHK(c, launch_xchg_min(a, flag, c->d_xmin, c->stream));
         HIPCHK(c, hipMemcpyAsync(&mn, c->d_xmin, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -711,7 +734,8 @@ void print_persist_trace(ksched_ctx *c) {
     auto at = [&](int64_t b, int col) { return t[(size_t)b * kTraceCols + col]; };
     double sum[16] = {};
     double scr[5] = {};  // WG 0 wave 0, screened batches: pass 1, bound merge, pass 2, exact phase (sums), exact rows
-    int64_t nscr = 0;
+    int64_t nscr = 0, npair = 0;
+    double pairs_sum = 0;  // WG 0: batches whose exact phase ran over the pair lists, and their pairs
     int64_t cnt = 0, first = -1, last = -1;
     constexpr int64_t L = kPipeLag;
     for (int64_t b = L; b < c->trace_cap; ++b) {
@@ -741,7 +765,9 @@ void print_persist_trace(ksched_ctx *c) {
             scr[1] += (double)(int64_t)(at(b, 12) - at(b, 11));
             scr[2] += (double)(int64_t)(at(b, 14) - at(b, 12));
             scr[3] += (double)(int64_t)(at(b, 8) - at(b, 14));
-            scr[4] += (double)at(b, 13);
+            scr[4] += (double)(uint32_t)at(b, 13);
+            const uint32_t pairs = (uint32_t)(at(b, 13) >> 32);
+            if (pairs != 0xffffffffu) { ++npair; pairs_sum += pairs; }
         }
     }
     if (c->d_dbg) {
@@ -778,9 +804,10 @@ void print_persist_trace(ksched_ctx *c) {
             sum[8] * us, sum[10] * us, sum[11] * us, sum[12] * us, sum[13] * us, sum[9] * us);
     if (nscr)
         fprintf(stderr, "persist screen (WG 0 wave 0): %lld of %lld batches screened | pass 1 %.2f us, bound %.2f us, "
-                "pass 2 %.2f us, exact rows %.2f us (%.2f of the workgroup's %d rows)\n", (long long)nscr, (long long)cnt,
+                "pass 2 %.2f us, exact phase %.2f us (%.2f of the workgroup's %d rows needed; pair lists in %lld batches, "
+                "%.1f pairs each)\n", (long long)nscr, (long long)cnt,
                 0.01 * scr[0] / nscr, 0.01 * scr[1] / nscr, 0.01 * scr[2] / nscr, 0.01 * scr[3] / nscr, scr[4] / nscr,
-                c->prog_rows);
+                c->prog_rows, (long long)npair, npair ? pairs_sum / (double)npair : 0.0);
 }
 
 constexpr int kXcds = 8;  // MI355X: 8 XCDs x 32 CUs
@@ -893,6 +920,7 @@ int enqueue_persistent(ksched_ctx *c) {
     // queues for a while must not turn into a spurious timeout)
     a.timeout_ticks = c->diag.persist_timeout_ms * 100000;
     a.no_screen = c->diag.no_screen ? 1 : 0;
+    a.no_pairs = c->diag.no_pairs ? 1 : 0;
     if (c->diag.trace) {
         const int64_t cap = 4 * (c->p / B) + 64;
         if (c->trace_cap < cap) {
@@ -1104,9 +1132,11 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.merge_stamps = env_int("KSCHED_MERGE_STAMPS", 0) != 0;
     c->diag.debug = env_int("KSCHED_DEBUG", 0) != 0;
     c->diag.no_screen = env_int("KSCHED_NO_SCREEN", 0) != 0;
+    c->diag.no_pairs = env_int("KSCHED_NO_PAIRS", 0) != 0;
     c->diag.poison = env_int("KSCHED_POISON", 0) != 0;
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
     c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
+    c->diag.epoch_base = env_int("KSCHED_XCHG_EPOCH_BASE", 0);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
     c->diag.rescue_rate = env_int("KSCHED_RESCUE_RATE", 4);
     c->diag.rescue_look = env_int("KSCHED_RESCUE_LOOK", 0);
@@ -1241,6 +1271,25 @@ int ksched_set_group(ksched_ctx *c, ksched_group *g) {
     return KSCHED_OK;
 }
 
+// The settings every rank of a node-sharded group must share, because every rank replays the same commit and takes
+// the same rescue-or-truncate decisions (the rescue policy) or lays out the same messages: carried in the handle
+// blob after the IPC handle and the epoch hint, checked by every importer (a rank with other
+// KSCHED_RESCUE_* settings would wait for rescue records no peer sends).
+constexpr int kPolicyWords = 8;
+constexpr size_t kPolicyOff = 72;
+static_assert(sizeof(hipIpcMemHandle_t) + 4 <= kPolicyOff && kPolicyOff + 4 * kPolicyWords <= KSCHED_XCHG_HANDLE_BYTES,
+              "handle blob layout");
+void policy_words(const ksched_ctx *c, uint32_t *w) {
+    w[0] = 0x4b534331u;  // "KSC1": a blob of this layout
+    w[1] = (uint32_t)c->diag.rescue_max;
+    w[2] = (uint32_t)c->diag.rescue_rate;
+    w[3] = (uint32_t)c->diag.rescue_cap;
+    w[4] = (uint32_t)c->diag.rescue_low;
+    w[5] = (uint32_t)c->diag.rescue_look;
+    w[6] = (uint32_t)c->B | (uint32_t)c->K << 16;
+    w[7] = (uint32_t)c->KC | (uint32_t)c->o.priority << 8 | (uint32_t)c->o.domain << 16 | (uint32_t)(c->o.use_labels != 0) << 24;
+}
+
 int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) {
     if (!c || !handle) return KSCHED_E_INVALID;
     const int R = c->o.nranks;
@@ -1262,6 +1311,9 @@ int ksched_xchg_export(ksched_ctx *c, uint8_t handle[KSCHED_XCHG_HANDLE_BYTES]) 
     std::memcpy(handle, &h, sizeof(h));
     const uint32_t hint = g_epoch_next.load();
     std::memcpy(handle + sizeof(h), &hint, sizeof(hint));
+    uint32_t pol[kPolicyWords];
+    policy_words(c, pol);
+    std::memcpy(handle + kPolicyOff, pol, sizeof(pol));
     return KSCHED_OK;
 }
 
@@ -1273,6 +1325,15 @@ int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
     const int R = c->o.nranks;
     rx_unmap_peers(c);
     c->xchg_ready = false;
+    {
+        uint32_t mine[kPolicyWords];
+        policy_words(c, mine);
+        for (int r = 0; r < R; ++r)
+            if (std::memcmp(handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES + kPolicyOff, mine, sizeof(mine)) != 0)
+                return fail(c, KSCHED_E_INVALID, "xchg_import: rank " + std::to_string(r) +
+                                                     " has other settings (batch, topk, priority, domain, labels or the "
+                                                     "KSCHED_RESCUE_* policy): every rank must share them");
+    }
     for (int r = 0; r < R; ++r) {
         if (r == c->o.rank) { c->rx_peer[r] = static_cast<char *>(c->d_rx); continue; }
         if (int rc = rx_map_peer(c, r, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES); rc != KSCHED_OK) {
@@ -1283,7 +1344,7 @@ int ksched_xchg_import(ksched_ctx *c, const uint8_t *handles) {
     // every ring was zeroed by its rank's export of this setup, before its handle left (rx_prepare), AND the tags
     // start at the largest hint of all ranks: beyond any tag any of their processes used, so no granule left in
     // reused memory can match (the same R blobs on every rank: the same epoch on every rank)
-    uint32_t e0 = 1;
+    uint32_t e0 = std::max<uint32_t>(1u, (uint32_t)c->diag.epoch_base);
     for (int r = 0; r < R; ++r) {
         uint32_t hint = 0;
         std::memcpy(&hint, handles + (size_t)r * KSCHED_XCHG_HANDLE_BYTES + sizeof(hipIpcMemHandle_t), sizeof(hint));
@@ -1314,9 +1375,11 @@ int ksched_xchg_join_local_ex(ksched_ctx *const *ctxs, int32_t n, int32_t flags)
         if (c->dev != c0->dev) return fail(c, KSCHED_E_INVALID, "xchg_join_local: the ranks must share one device");
         if (c->B > 64) return fail(c, KSCHED_E_INVALID, "xchg_join_local: the persistent pipeline needs batch <= 64");
         if (c->group) return fail(c, KSCHED_E_STATE, "xchg_join_local: context uses an in-process rank group");
-        if (c->B != c0->B || c->K != c0->K || c->KC != c0->KC || c->o.priority != c0->o.priority ||
-            c->o.domain != c0->o.domain || c->o.use_labels != c0->o.use_labels)
-            return fail(c, KSCHED_E_INVALID, "xchg_join_local: the ranks' options differ");
+        uint32_t pc[kPolicyWords], p0[kPolicyWords];
+        policy_words(c, pc);
+        policy_words(c0, p0);
+        if (std::memcmp(pc, p0, sizeof(pc)) != 0)
+            return fail(c, KSCHED_E_INVALID, "xchg_join_local: the ranks' options or rescue policies differ");
     }
     auto g = std::make_shared<ksched_lgroup>();
     g->R = n;
@@ -1355,7 +1418,7 @@ int ksched_xchg_join_local_ex(ksched_ctx *const *ctxs, int32_t n, int32_t flags)
         }
     }
     // the same epoch rule as xchg_import: the process's first unused tag (one process: one hint)
-    const uint32_t e0 = (c0->diag.xchg_diag & 2) ? 1u : std::max<uint32_t>(1u, g_epoch_next.load());  // 2: round 4's tags
+    const uint32_t e0 = (c0->diag.xchg_diag & 2) ? 1u : std::max<uint32_t>({1u, g_epoch_next.load(), (uint32_t)c0->diag.epoch_base});
     epoch_used_below(e0 + 1);
     for (int r = 0; r < n; ++r) {
         ksched_ctx *c = ctxs[r];
@@ -1873,7 +1936,10 @@ static int sync_impl(ksched_ctx *c) {
         // every rank counted the same active batches and rescues (batch tags epoch0 + a, rescue tags epoch0 + q):
         // the next call's tags start past this call's, and this process never uses them again
         const Ctl *h = reinterpret_cast<const Ctl *>(c->h_cursor);
-        c->xchg_epoch += (uint32_t)h->nact + (uint32_t)h->stats[4] + 2u;
+        // (a step of a multiple of 2^15 would give the next call's barrier granules the tag of this call's:
+        // gran_tag keeps 15 bits -- skip one more)
+        const uint32_t step = (uint32_t)h->nact + (uint32_t)h->stats[4] + 2u;
+        c->xchg_epoch += step + ((step & 0x7fffu) == 0 ? 1u : 0u);
         epoch_used_below(c->xchg_epoch);
         if (e) c->xchg_ready = false;  // the rings' state is unknown: later calls take the RCCL path
         c->xchg_run = false;

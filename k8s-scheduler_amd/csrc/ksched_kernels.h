@@ -462,6 +462,7 @@ struct PersistArgs {
     int32_t *err;           // device error word (5..9 = a persistent wait timed out)
     int64_t timeout_ticks;
     int32_t no_screen;      // diagnostics (KSCHED_NO_SCREEN): the exact scan in every batch
+    int32_t no_pairs;       // diagnostics (KSCHED_NO_PAIRS): the screened scan's exact phase by rows, never by pairs
     int32_t screen_ok;      // the screened scan's reciprocals fit in a score workgroup's LDS
     int32_t screen_h;       // ... and so do pass 1's per-pair records
     // optional (KSCHED_PERSIST_TRACE): wall-clock stamps per batch, [trace_cap][kTraceCols]
@@ -498,7 +499,7 @@ struct PersistArgs {
     int32_t rescue_max;     // rescues per batch before an exhausted list truncates it (KSCHED_RESCUE_MAX)
     int32_t rescue_cap;     // the rescue bucket's capacity in rescues (KSCHED_RESCUE_CAP, default rescue_max)
     int32_t rescue_low;     // rescues per batch while the bucket is below half full (KSCHED_RESCUE_LOW)
-    int32_t rescue_look;    // KSCHED_RESCUE_LOOK (default 1): the commit's look-ahead over the batch's exhausted lists
+    int32_t rescue_look;    // KSCHED_RESCUE_LOOK (default 0): the commit's look-ahead over the batch's exhausted lists
     int32_t rescue_rate;    // the commit workgroup's rescue bucket refill per batch, quarter rescues (KSCHED_RESCUE_RATE)
     int32_t touch_screen;   // the commit's touched-node screen (KSCHED_NO_TOUCH_SCREEN=1: every key exact)
     // the merger slots' keys of their pod against the entries of export(b - 2), which commit(b) inherits:
@@ -572,7 +573,9 @@ __device__ __forceinline__ bool poll_ge(const unsigned long long *p, unsigned lo
 // bits 0..15} low, {tag16 | word bits 16..31} high, tag16 = (tag & 0x7fff) | 0x8000 (never 0: a zeroed ring holds no
 // live granule).  A reader accepts the granule only when both halves carry the tag, so a granule read half old and
 // half new (an 8-byte access split into two 4-byte ones -- seen on uncached rings) is never
-// taken for the new one.  Tags 32768 apart would alias; a ring region is rewritten every 4 active batches.
+// taken for the new one.  Tags 32768 apart would alias: every call zeroes the message and rescue areas before its
+// rank barrier (ksched_engine.hip rx_zero_regions), within a call a region is rewritten every 4 active batches, and
+// consecutive calls' barrier tags never differ by a multiple of 2^15.
 __device__ __forceinline__ uint32_t gran_tag(uint32_t tag) { return (tag & 0x7fffu) | 0x8000u; }
 __device__ __forceinline__ uint64_t gran_enc(uint32_t word, uint32_t t16) {
     return ((uint64_t)((t16 << 16) | (word >> 16)) << 32) | (uint64_t)((t16 << 16) | (word & 0xffffu));

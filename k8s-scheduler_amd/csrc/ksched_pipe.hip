@@ -47,13 +47,32 @@ constexpr int kPU = 4;                 // rows per score step (independent key c
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0
 #endif
-#ifndef KSCHED_REC_PKRTZ
-#define KSCHED_REC_PKRTZ 1  // pass 1's two records per v_cvt_pkrtz_f16_f32
-#endif
 #ifndef KSCHED_SCREEN_PU
 #define KSCHED_SCREEN_PU 4
 #endif
 constexpr int kSPU = KSCHED_SCREEN_PU;  // rows per step of the screened scan's passes
+// The screened scan's exact phase over (row, pod) pairs: each pod's needed rows (at most kPairCap; ~4-8 on c4) and
+// the batch's pairs (at most kPairMax) -- past either the batch takes the row path (every needed row for every pod)
+constexpr int kPairCap = 48;
+constexpr int kPairMax = 1024;
+
+// ds_bpermute: lane `src`'s value of v (every lane of the wave must be active)
+__device__ __forceinline__ int bperm(int v, int src) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ int64_t bperm64(int64_t v, int src) {
+    const uint32_t lo = (uint32_t)bperm((int)(uint32_t)(uint64_t)v, src);
+    const uint32_t hi = (uint32_t)bperm((int)(uint32_t)((uint64_t)v >> 32), src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+// inclusive prefix sum over the wave's lanes (Hillis-Steele; every lane active)
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    const int lane = (int)__lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = bperm(v, lane >= d ? lane - d : 0);
+        v += lane >= d ? t : 0;
+    }
+    return v;
+}
 
 // ---- barrier of ONE role's waves (LDS counter; s_barrier would wait for the other role too) ----------
 __device__ __forceinline__ void role_sync(unsigned *ctr, unsigned &target, unsigned nwaves) {
@@ -73,6 +92,7 @@ struct alignas(16) PipeCtl {
     int32_t c_stop;               // commit workgroup
     int32_t s_ex;                 // score role: rows of this batch scored exactly (screened scan)
     int32_t s_scr;                // score role: this batch uses the screened scan
+    int32_t s_pairs;              // score role: pairs scored exactly (pair lists), -1: the row path
     // score role: the next batch's loads and export apply, done by wave kSW - 1 during this batch's fold
     int32_t n_ok, n_err;          // n_ok: they were (commit(b + 1 - kPipeLag) was already published)
     int64_t n_p0, n_done;
@@ -302,6 +322,20 @@ struct ScoreLayout {
     __host__ __device__ static int hrec_qw(int R) { return ((R + kSW - 1) / kSW + 1) / 2 * 2; }
     __host__ __device__ static size_t hrec_bytes(int R) { return (size_t)kSW * hrec_qw(R) * 64 * 2; }
     __host__ __device__ static size_t total_with_hrec(int R) { return total_screen(R) + hrec_bytes(R); }
+    // the pair lists (score_role's exact phase), inside the fold area after the screened scan's bound lists, queue
+    // counts and row queues, in front of s_cnt: cnt[64] u32, nel[64] u32, key[kPairMax] f64, row[64][kPairCap] u16
+    __host__ __device__ static size_t pair_off(int R) {
+        const size_t QW = (size_t)(R + kSW - 1) / kSW;
+        return ((size_t)kSW * KC * 64 * 4 + kSW * 4 + 4 * kSW * QW + 15) / 16 * 16;
+    }
+    static constexpr size_t pair_bytes = 64 * 4 * 2 + (size_t)kPairMax * 8 + (size_t)64 * kPairCap * 2;
+    __host__ __device__ static bool pairs_fit(int R) { return pair_off(R) + pair_bytes <= (size_t)kSW * KC * 64 * 12; }
+};
+struct PairArea {
+    uint32_t *cnt;  // [64] needed rows per pod (atomic; past kPairCap: the batch takes the row path)
+    uint32_t *nel;  // [64] eligible keys per pod
+    double *key;    // [kPairMax] the pairs' exact keys (-inf: no key), pod-major
+    uint16_t *row;  // [64][kPairCap] the needed rows of each pod
 };
 
 // LDS of a merger workgroup: kMS slots of {control words | merge scratch | exchange messages}
@@ -344,6 +378,14 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     float4 *ysq = reinterpret_cast<float4 *>(smem + ScoreLayout<KC, K>::ysq_off(R));  // screen reciprocals, SoA rows
     uint16_t *hrec = reinterpret_cast<uint16_t *>(smem + ScoreLayout<KC, K>::hrec_off(R));  // [kSW][QW/2][64] u16 pairs (P.screen_h)
     int32_t *s_cnt = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 12);  // [64], after the fold lists
+    PairArea pr;
+    {
+        char *pa = fold + ScoreLayout<KC, K>::pair_off(R);
+        pr.cnt = reinterpret_cast<uint32_t *>(pa);
+        pr.nel = pr.cnt + 64;
+        pr.key = reinterpret_cast<double *>(pa + 512);
+        pr.row = reinterpret_cast<uint16_t *>(pa + 512 + (size_t)kPairMax * 8);
+    }
     constexpr int kST = kSW * 64;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -372,6 +414,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     // some pod of the batch, its f32 screen cannot prove the pair below the workgroup's KC-th best key;
     // each workgroup turns it off for a while when most of its rows need the exact score anyway
     constexpr bool kScreen = PRIO == kPrioResource && F53;
+    // the exact phase over (row, pod) pairs (PairArea) when the lists fit the fold area; else every needed row is
+    // scored for every pod (the row path)
+    constexpr bool kPairs = kScreen;
+    const bool pairs_ok = kPairs && !P.no_pairs && ScoreLayout<KC, K>::pairs_fit(R);
     constexpr int kScreenOffBatches = 16;
     constexpr bool kPrefetch = kSW > 8 && KSCHED_SCORE_PREFETCH;  // wave kSW - 1 does not fold
     int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
@@ -495,6 +541,9 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
         const uint64_t t_go = ((P.trace || P.trace_wg) && tid == 0) ? wall_clock64() : 0;
         // ---- score: lane = pod, wave w scans rows r = w, w + W, ... (nodes j = g + r G) ----
         if (tid < 64) s_cnt[tid] = 0;
+        if (kPairs && tid < 64) { pr.cnt[tid] = 0; pr.nel[tid] = 0; }
+        bool pairs = false;          // this batch's exact phase runs over the pair lists
+        int pT = 0, pincl = 0, pexcl = 0;  // ... pairs in all, and lane (pod) p's range [pexcl, pincl)
         const int64_t pod = p0 + lane;
         const bool active = (lane < P.B) && (pod < NP);
         const int64_t rc = active ? P.pods.rc[pod] : 0;
@@ -561,10 +610,8 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                     uint32_t xs[kSPU];
                     uint32_t hh[kSPU];
                     uint32_t ambm = 0;  // rows of this group with an ambiguous fraction for this lane's pod
-#if KSCHED_REC_PKRTZ
-                    float vv[kSPU];
-                    bool nrm[kSPU];
-#endif
+                    float ww[kSPU];     // the record's w before its conversion: base - v (screen_rec / screen_rec_nf)
+                    uint32_t nrm[kSPU]; // 0: the record is hh; 1: a resource-fitting record; 0x8000 | 1: non-fitting
 #pragma unroll
                     for (int u = 0; u < kSPU; ++u) {
                         const int r = r0 + u * kSW;
@@ -578,30 +625,22 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const float v = screen_q(c, m, p, okc, okm, okp, &lo_ok);
                         cnt += (valid && f && !amb) ? 1 : 0;
                         xs[u] = (valid && active && el && lo_ok && !amb) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
-                        // the pair's upper bound (screen_rec): 0 (always needed) when ambiguous, 0xffff (never
-                        // needed) without a key
-#if KSCHED_REC_PKRTZ
-                        vv[u] = v;
-                        nrm[u] = !amb && el;
+                        // the pair's upper bound (screen_rec / screen_rec_nf by the screen's form): 0 (always needed)
+                        // when ambiguous, 0xffff (never needed) without a key
+                        const bool rf = okc & okm & okp;
+                        ww[u] = __builtin_fmaxf((rf ? 10.0f : kNfBase) - v, 0.0f);
+                        nrm[u] = (!amb && el) ? (rf ? 1u : 0x8001u) : 0u;
                         hh[u] = amb ? 0u : 0xffffu;
-#else
-                        hh[u] = amb ? 0u : (el ? screen_rec(v) : 0xffffu);
-#endif
                         ambm |= (valid && amb) ? 1u << u : 0u;
                     }
                     // the records of rows k, k + 1 (k = (r0 - wave) / kSW + u, u even) in one store; a pair's second
                     // row past the wave's last is never read
 #pragma unroll
                     for (int u = 0; u < kSPU; u += 2) {
-#if KSCHED_REC_PKRTZ
-                        // both rows' screen_rec in one conversion: round toward zero IS its round-down for w >= 0
-                        const uint32_t rec = __builtin_bit_cast(
-                            uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_fmaxf(10.0f - vv[u], 0.0f),
-                                                                 __builtin_fmaxf(10.0f - vv[u + 1], 0.0f)));
-                        const uint32_t w2 = (nrm[u] ? (rec & 0xffffu) : hh[u]) | ((nrm[u + 1] ? (rec >> 16) : hh[u + 1]) << 16);
-#else
-                        const uint32_t w2 = hh[u] | (hh[u + 1] << 16);
-#endif
+                        // both rows' records in one conversion: round toward zero IS the records' round-down for w >= 0
+                        const uint32_t rec = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(ww[u], ww[u + 1]));
+                        const uint32_t w2 = (nrm[u] ? ((rec & 0xffffu) | (nrm[u] & 0x8000u)) : hh[u]) |
+                                            ((nrm[u + 1] ? ((rec >> 16) | (nrm[u + 1] & 0x8000u)) : hh[u + 1]) << 16);
                         if (r0 + u * kSW < Rv) hw[(size_t)(((r0 - wave) / kSW + u) / 2) * 64] = w2;
                     }
                     if (__ballot(ambm != 0)) {  // wave-uniform, rare: queue the rows with an ambiguous pair
@@ -661,15 +700,26 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             }
             const float L = __uint_as_float(t[KC - 1]);  // + 1; 0 = fewer than KC bounds: everything passes
             if (g == 0 && tid == 0) trace_at(P, b, 12);
+            // the predicate counts (s_cnt was zeroed before pass 1, and that write is ordered by the barrier above)
+            if (cnt) atomicAdd(&s_cnt[lane], cnt);
             // ---- pass 2: a row needs its exact scores when some pod's upper bound reaches L (a pair below
             // L is below KC eligible keys of this workgroup, so it is in no top-KC list the exact scan would
-            // have produced); the wave queues such rows ----
+            // have produced); the wave queues such rows, and (pair lists) each needed (row, pod) pair in its
+            // pod's list ----
             int qn = 0;
+            // pod `lane` needs row r: one slot of its pair list (a count past kPairCap sends the batch to the row path)
+            auto add_pair = [&](bool need, int r) {
+                if (kPairs && need) {
+                    const uint32_t s = atomicAdd(&pr.cnt[lane], 1u);
+                    if (s < (uint32_t)kPairCap) pr.row[lane * kPairCap + s] = (uint16_t)r;
+                }
+            };
             if (keep_h) {
                 const int nr = (Rv - wave + kSW - 1) / kSW;  // this wave's rows
                 // in the records' own units: the pair is needed when its bound + 1 + eps reaches L; -1: an
                 // inactive lane
                 const int tq = active ? screen_rec_threshold(L) : -1;
+                const int tqn = active ? screen_rec_threshold_nf(L) : -1;
                 for (int i0 = 0; i0 < nr; i0 += 8) {
                     uint16_t hv[8];
 #pragma unroll
@@ -678,11 +728,14 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         hv[u] = (uint16_t)x;
                         hv[u + 1] = (uint16_t)(x >> 16);
                     }
-                    uint32_t grp = 0;  // wave-uniform: the group's rows some pod needs
+                    uint32_t grp = 0;   // wave-uniform: the group's rows some pod needs
+                    uint32_t mine = 0;  // ... and the ones this lane's pod needs
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
-                        const uint64_t bm = __builtin_amdgcn_ballot_w64((int)hv[u] <= tq);
+                        const bool nd = screen_rec_needed(hv[u], tq, tqn);
+                        const uint64_t bm = __builtin_amdgcn_ballot_w64(nd);
                         grp |= (bm != 0 ? 1u : 0u) << u;
+                        mine |= (nd ? 1u : 0u) << u;
                     }
                     if (nr - i0 < 8) grp &= (1u << (nr - i0)) - 1u;  // rows past the wave's last
                     // lanes 0..7 queue the group's needed rows in order, one store (a wave's rows fit its QW)
@@ -690,6 +743,14 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         qrow[wave * QW + qn + __builtin_popcount(grp & ((1u << lane) - 1u))] =
                             (uint16_t)(wave + (i0 + lane) * kSW);
                     qn += __builtin_popcount(grp);
+                    if (kPairs && grp) {  // one slot reservation per lane for the group's needed rows
+                        uint32_t mm = mine & grp;
+                        const int c = __builtin_popcount(mm);
+                        uint32_t s = c ? atomicAdd(&pr.cnt[lane], (uint32_t)c) : 0u;
+                        for (; mm; mm &= mm - 1u, ++s)
+                            if (s < (uint32_t)kPairCap)
+                                pr.row[lane * kPairCap + s] = (uint16_t)(wave + (i0 + __builtin_ctz(mm)) * kSW);
+                    }
                 }
             } else {
                 for (int r0 = wave; r0 < Rv; r0 += kSW * kSPU) {
@@ -709,17 +770,52 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                         const bool any = __ballot(need) != 0;
                         if (lane == 0 && qn < QW) qrow[wave * QW + qn] = (uint16_t)r;  // kept when any
                         qn += any ? 1 : 0;
+                        if (any) add_pair(need, r);
                     }
                 }
             }
             if (lane == 0) qcnt[wave] = qn;
             if (g == 0 && tid == 0) trace_at(P, b, 14);
             sync();
-            // ---- the queued rows, dealt round-robin to the waves (balanced), scored exactly for every pod;
-            // arrival order is not node order, so the insert ranks ties by node index ----
             int base[kSW], tot = 0;
 #pragma unroll
             for (int w = 0; w < kSW; ++w) { base[w] = tot; tot += qcnt[w]; }
+            // ---- the pair lists (every wave computes the same prefix over the pods' counts, lane = pod): when
+            // none overflowed, thread e scores the e-th needed (row, pod) pair exactly -- ~4-8 pairs per pod
+            // instead of every pod against every needed row ----
+            if (kPairs) {
+                const int c = (int)pr.cnt[lane];
+                pincl = wave_incl_sum(c);
+                pexcl = pincl - c;
+                pT = __builtin_amdgcn_readlane(pincl, 63);
+                pairs = pairs_ok && __ballot(c > kPairCap) == 0 && pT <= kPairMax;  // workgroup-uniform
+            }
+            if (pairs) {
+                for (int e0 = wave * 64; e0 < pT; e0 += kST) {  // wave-uniform trip count: every lane shuffles
+                    const int e = e0 + lane;
+                    const int ec = e < pT ? e : pT - 1;
+                    int p = 0;  // the pod: how many lanes' inclusive counts are <= e
+#pragma unroll
+                    for (int st = 32; st; st >>= 1) p += bperm(pincl, p + st - 1) <= ec ? st : 0;
+                    const int s = ec - bperm(pexcl, p);
+                    const int64_t qc = bperm64(rc, p), qm = bperm64(rm, p), qp = bperm64(rp, p);
+                    const uint64_t qs = LAB ? (uint64_t)bperm64((int64_t)sel, p) : 0ull;
+                    if (e < pT) {
+                        const int r = pr.row[p * kPairCap + s];
+                        const NodeRec &nd = rows[r];
+                        const int64_t ac = nd.a[0], am = nd.a[1], ap = nd.a[2];
+                        const bool f = fits(qc, qm, qp, qs, ac, am, ap, nd.labels, LAB);
+                        double k;
+                        const bool el = pair_key_fast<PRIO, DOM, F53>(f, qc, qm, qp, (double)qc, (double)qm, (double)qp, ac,
+                                                                      am, ap, nd.af[0], nd.af[1], nd.af[2], nd.y[0],
+                                                                      nd.y[1], nd.y[2], y3, nd.price, &k);
+                        pr.key[e] = el ? k : -__builtin_inf();
+                        if (el) atomicAdd(&pr.nel[p], 1u);
+                    }
+                }
+            } else
+            // ---- the queued rows, dealt round-robin to the waves (balanced), scored exactly for every pod;
+            // arrival order is not node order, so the insert ranks ties by node index ----
             for (int e = wave; e < tot; e += kSW) {
                 int w = 0;
 #pragma unroll
@@ -733,7 +829,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                                                               nd.af[2], nd.y[0], nd.y[1], nd.y[2], y3, nd.price, &k);
                 if (el) list_insert_ordered<KC>(key, idx, k, (int32_t)(P.node_offset + g + (int64_t)r * G));
             }
-            if (wave == 0 && lane == 0) pc->s_ex = tot;
+            if (wave == 0 && lane == 0) { pc->s_ex = tot; pc->s_pairs = pairs ? pT : -1; }
         } else
         // kPU rows per step: their keys are independent f64 chains the scheduler interleaves; inserted
         // in ascending node order afterwards
@@ -781,26 +877,10 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             pre_c = __hip_atomic_load(&ctl->committed_x[g % kCtlReplicas].v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sync();  // every wave's scan is done (the fold area is free); s_cnt was zeroed
         if (g == 0 && tid == 0) trace_at(P, b, 9);
-        if (cnt) atomicAdd(&s_cnt[lane], cnt);
-        // ---- fold: every wave's lists to LDS; then wave w merges pods 8w .. 8w+7 for all 8 source waves at
-        // once (lane = pod x source wave; three 8-lane butterfly merges of sorted lists) and stores them.  A
-        // list that is cut when full folds into the top-KC of the union, again cut when full (DESIGN.md 4).
-        double *fk = reinterpret_cast<double *>(fold);                                  // [kSW][KC][64]
-        int32_t *fi = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 8);    // [kSW][KC][64]
-#pragma unroll
-        for (int q = 0; q < KC; ++q) {
-            fk[(wave * KC + q) * 64 + lane] = key[q];
-            fi[(wave * KC + q) * 64 + lane] = idx[q];
-        }
-        sync();
-        static_assert(kSW >= 8 && kSW <= 16, "the fold deals 8 pods to each of the first 8 waves");
-        const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch (waves 0..7)
-        const int src = lane & 7;               // ... and source wave (plus src + 8 when that exists)
-        const bool folds = wave < 8;
-        if (kPrefetch && wave == kSW - 1) {
-            // ---- the next batch's loads and export apply, while waves 0..7 fold: a workgroup still busy
-            // with this batch when commit(b + 1 - kPipeLag) is published starts the next scan right after
-            // its arrival.  Only when that commit is already out: this wave never waits for it ----
+        // ---- the next batch's loads and export apply by wave kSW - 1, while the others fold (or rank the pairs): a
+        // workgroup still busy with this batch when commit(b + 1 - kPipeLag) is published starts the next scan right
+        // after its arrival.  Only when that commit is already out: this wave never waits for it ----
+        auto prefetch_next = [&]() {
             const unsigned long long need = (unsigned long long)(b + 1 - kPipeLag + 1);
             int ok = 0;
             if (lane == 0) {
@@ -817,7 +897,82 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 if (lane == 0) { pc->n_p0 = p0v; pc->n_done = donev; pc->n_err = errv; }
             }
             if (lane == 0) pc->n_ok = ok;
+        };
+        const size_t part_elems = (size_t)P.B * G;
+        Cand *part = P.part + (size_t)(b % kPipeLag) * part_elems * KC;  // merge(b) is done before score(b + kPipeLag)
+        // entry q of pod pl's list as one 16-B record {key, idx, pad}, entry 0's pad carrying the workgroup's predicate
+        // count for the pod; word 3: the batch's tag (bits 16..31) and, in entry 0, the count (< 2^16 rows per workgroup)
+        auto store_entry = [&](int pl, int q, double kk, int32_t ii) {
+            const uint64_t kb = (uint64_t)__double_as_longlong(kk);
+            const uint32_t tag = (uint32_t)((b + 1) & 0xffff) << 16;
+            const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, tag | (q == 0 ? (uint32_t)s_cnt[pl] : 0u)};
+            st_coh16(coh_rsrc(part), (uint32_t)((((size_t)pl * G + g) * KC + q) * sizeof(Cand)), v);
+        };
+        if (pairs) {
+            // ---- pair lists: each scored pair's rank among its pod's pairs (key desc, node index asc -- rows are in
+            // node order within the workgroup) is its slot; the KC best are stored, wave 0 fills the empty slots ----
+            if (kPrefetch && wave == kSW - 1) {
+                prefetch_next();
+            } else {
+                constexpr int RW = kPrefetch ? kSW - 1 : kSW;  // the ranking waves
+                for (int e0 = wave * 64; e0 < pT; e0 += RW * 64) {  // wave-uniform trip count: every lane shuffles
+                    const int e = e0 + lane;
+                    const int ec = e < pT ? e : pT - 1;
+                    int p = 0;
+#pragma unroll
+                    for (int st = 32; st; st >>= 1) p += bperm(pincl, p + st - 1) <= ec ? st : 0;
+                    const int ex = bperm(pexcl, p), in = bperm(pincl, p);
+                    if (e < pT) {
+                        const double k = pr.key[e];
+                        if (k != -__builtin_inf()) {
+                            const uint16_t *prow = pr.row + p * kPairCap;
+                            const int r = prow[e - ex];
+                            int rank = 0;
+                            int e2 = ex;
+                            for (; e2 + 4 <= in; e2 += 4) {  // four loads in flight
+                                double k2[4];
+                                int r2[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) { k2[u] = pr.key[e2 + u]; r2[u] = prow[e2 + u - ex]; }
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) rank += (k2[u] > k || (k2[u] == k && r2[u] < r)) ? 1 : 0;
+                            }
+                            for (; e2 < in; ++e2) {
+                                const double k2 = pr.key[e2];
+                                const int r2 = prow[e2 - ex];
+                                rank += (k2 > k || (k2 == k && r2 < r)) ? 1 : 0;
+                            }
+                            if (rank < KC && p < P.B && p0 + p < NP)
+                                store_entry(p, rank, k, (int32_t)(P.node_offset + g + (int64_t)r * G));
+                        }
+                    }
+                }
+                if (wave == 0 && lane < P.B && p0 + lane < NP) {
+                    for (int q = (int)pr.nel[lane]; q < KC; ++q) store_entry(lane, q, -__builtin_inf(), kNoIdx);
+                }
+            }
+            if (g == 0 && tid == 0) trace_at(P, b, 10);
+            // Wave 0's export apply (the node rows the mergers read for the candidates' state) complete before the
+            // arrival, independent of what follows
+            if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+        if (!scr && cnt) atomicAdd(&s_cnt[lane], cnt);  // (screened batches counted after pass 1)
+        // ---- fold: every wave's lists to LDS; then wave w merges pods 8w .. 8w+7 for all 8 source waves at
+        // once (lane = pod x source wave; three 8-lane butterfly merges of sorted lists) and stores them.  A
+        // list that is cut when full folds into the top-KC of the union, again cut when full (DESIGN.md 4).
+        double *fk = reinterpret_cast<double *>(fold);                                  // [kSW][KC][64]
+        int32_t *fi = reinterpret_cast<int32_t *>(fold + (size_t)kSW * KC * 64 * 8);    // [kSW][KC][64]
+#pragma unroll
+        for (int q = 0; q < KC; ++q) {
+            fk[(wave * KC + q) * 64 + lane] = key[q];
+            fi[(wave * KC + q) * 64 + lane] = idx[q];
         }
+        sync();
+        static_assert(kSW >= 8 && kSW <= 16, "the fold deals 8 pods to each of the first 8 waves");
+        const int pl = wave * 8 + (lane >> 3);  // this lane's pod of the batch (waves 0..7)
+        const int src = lane & 7;               // ... and source wave (plus src + 8 when that exists)
+        const bool folds = wave < 8;
+        if (kPrefetch && wave == kSW - 1) prefetch_next();
         if (folds) {
 #pragma unroll
             for (int q = 0; q < KC; ++q) {
@@ -837,14 +992,11 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
             fold_stage<2, KC>(key, idx);
         }
         if (g == 0 && tid == 0) trace_at(P, b, 10);
-        const size_t part_elems = (size_t)P.B * G;
-        Cand *part = P.part + (size_t)(b % kPipeLag) * part_elems * KC;  // merge(b) is done before score(b + kPipeLag)
         // Wave 0's export apply (the node rows the mergers read for the candidates' state) complete before the
         // arrival: drained here, a whole scan after it was issued (free by now), independent of what follows
         if (wave == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (folds && pl < P.B && p0 + pl < NP && src < KC) {
-            // every lane of the group holds the pod's list: lane src stores entry src as one 16-B record
-            // {key, idx, pad}, entry 0's pad carrying the workgroup's predicate count for the pod
+            // every lane of the group holds the pod's list: lane src stores entry src
             double kk = key[0];
             int32_t ii = idx[0];
 #pragma unroll
@@ -852,18 +1004,16 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                 kk = src == q ? key[q] : kk;
                 ii = src == q ? idx[q] : ii;
             }
-            const uint64_t kb = (uint64_t)__double_as_longlong(kk);
-            // word 3: the batch's tag (bits 16..31) and, in entry 0, the count (< 2^16 rows per workgroup)
-            const uint32_t tag = (uint32_t)((b + 1) & 0xffff) << 16;
-            const u32x4 v = {(uint32_t)kb, (uint32_t)(kb >> 32), (uint32_t)ii, tag | (src == 0 ? (uint32_t)s_cnt[pl] : 0u)};
-            st_coh16(coh_rsrc(part), (uint32_t)((((size_t)pl * G + g) * KC + src) * sizeof(Cand)), v);
+            store_entry(pl, src, kk, ii);
+        }
         }
         // The records need no drain (the mergers read them again until their tags are this batch's)
         sync();  // every wave's record stores issued
         if (wave == 0) {
             // most rows needed the exact score: the screen only costs here -- scan unscreened for a while
             if (scr && 2 * pc->s_ex > R) scr_off_until = b + 1 + kScreenOffBatches;
-            if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap) P.trace[b * kTraceCols + 13] = (uint64_t)pc->s_ex;
+            if (scr && g == 0 && lane == 0 && P.trace && b < P.trace_cap)  // rows | pairs << 32 (0xffffffff: row path)
+                P.trace[b * kTraceCols + 13] = (uint64_t)(uint32_t)pc->s_ex | (uint64_t)(uint32_t)pc->s_pairs << 32;
             if (lane == 0) { ex_rows += scr ? pc->s_ex : Rvalid; scan_rows += Rvalid; }
             // ---- arrive (the merge waves of workgroups 1 .. B wait for all G) ----
             jitter_at(P.jitter, b, 2);
@@ -1130,8 +1280,8 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
         ++nact;
         const int slot = (int)((nact - 1) % 4);
         const unsigned long long use = (unsigned long long)((nact - 1) / 4);
-        // the pods' keys against the older inherited export, while the score workgroups still scan the batch
-        // (commit(b - 2) usually ends well before the batch's last arrival): off the merge -> commit path
+        // the pods' keys against the older inherited export, while the score workgroups still scan the batch: off
+        // the merge -> commit path (after the merge instead, c4 measured 10 % slower: the merges then end later)
         if (P.inh && b >= 2) {
             if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit)) return;
             jitter_at(P.jitter, b, 3);
@@ -1351,7 +1501,8 @@ __device__ __forceinline__ void commit_role(const PersistArgs &P, char *smem, co
                     const uint64_t t0 = wall_clock64();
                     for (int it = 1;; ++it) {
                         const u32x4 c0 = ld_coh16(hr, 0), c1 = ld_coh16(hr, 16);  // one address: one request
-                        const bool eok = load_xrec_pipe(xin_e, lane, tag, xo);
+                        // (lanes past the export slot's 2B entries load nothing: the buffer resource does not bound them)
+                        const bool eok = lane < 2 * P.B ? load_xrec_pipe(xin_e, lane, tag, xo) : true;
                         const bool hok = __builtin_amdgcn_readfirstlane((int)(c0.x == tag && c1.x == tag)) != 0;
                         const int n1 = hok ? (int)__builtin_amdgcn_readfirstlane((int)c0.y) : 64;
                         if (hok && __ballot(lane < n1 && !eok) == 0) {

@@ -111,7 +111,8 @@ def test_xchg_eight_ranks_c4_full_nodes(gpu_available, oracle_mod):
 def test_xchg_groups_in_one_process_uncached(gpu_available, oracle_mod):
     """Several groups in ONE process over uncached rings, in the order that failed in round 4 (two-rank groups,
     a three-rank group, then a two-rank group whose rings can land where the earlier groups' were): each group's
-    rings are zeroed at its setup and its tags start at 1, so no group may see an earlier group's granules."""
+    rings are zeroed at its setup and its tags start past every tag this process used, so no
+    group may see an earlier group's granules."""
     from ksched import cluster
     for cfg, nn, pp, world in (("c3", 24000, 3000, 2), ("c4", 30000, 2500, 3), ("c4", 100000, 2500, 2),
                                ("c3", 24000, 3000, 2)):
@@ -122,7 +123,8 @@ def test_xchg_groups_in_one_process_uncached(gpu_available, oracle_mod):
 
 def test_xchg_rejoin_reuses_rings(gpu_available, oracle_mod):
     """One group joined, run, joined AGAIN (the same contexts: the rings are reused, zeroed again and the tags
-    restart at 1 -- the rule of a second ksched_xchg_export/import) and run again: bit-exact both times."""
+    start past the process's used ones -- the rule of a second ksched_xchg_export/import) and run again: bit-exact
+    both times."""
     from ksched import cluster
     from ksched.dist import make_local_xchg_group
     from ksched.engine import Engine
@@ -181,3 +183,69 @@ def test_xchg_sharded_rescue(gpu_available, oracle_mod, world):
           f"{one['truncations']} truncated")
     assert nres > 0, f"no rescue in {world} ranks (one rank: {one['rescues']} rescues, {one['truncations']} truncated)"
     assert ntr <= 2 * one["truncations"] + 2, f"{world} ranks truncated {ntr} batches, one rank {one['truncations']}"
+
+
+def test_xchg_tags_wrap_across_calls(gpu_available, oracle_mod, monkeypatch):
+    """Granule tags keep 15 bits (ksched_kernels.h gran_tag).  Tags started just below 2^15 (KSCHED_XCHG_EPOCH_BASE)
+    cross the wrap during these calls, and calls with rescues alternate with short calls that write only some
+    message slots and no rescue area: every call zeroes its ring's message and rescue areas before the rank barrier
+    (ksched_engine.hip rx_zero_regions), so no wait can take an earlier call's granule.  Bit-exact."""
+    from ksched import cluster
+    from ksched.dist import make_local_xchg_group
+    from ksched.engine import Engine
+    monkeypatch.setenv("KSCHED_XCHG_EPOCH_BASE", str(32768 - 150))
+    big = cluster.make_cluster("c4", n_nodes=100000, n_pods=6000)   # ~100 active batches and rescues per call
+    small = big.subset_pods(70)                                    # two active batches, no rescue
+    want_big = oracle_mod.schedule(big, nthreads=8)
+    want_small = oracle_mod.schedule(small, nthreads=8)
+    ranks = make_local_xchg_group(big, 2, device=0, topk=16, batch=64, rings="uncached")
+    try:
+        for e, _ in ranks:
+            e.save_state()
+        for rep in range(3):
+            check_oracle(big, run_local(big, 2, calls=1, engines=ranks), want_big, 2)
+            check_oracle(small, run_local(small, 2, calls=2, engines=ranks), want_small, 2)
+    finally:
+        Engine.close_group([e for e, _ in ranks])
+
+
+def _full_c4_sharded(world, batch):
+    """All 1M c4 pods at the full 100k nodes on `world` local ranks (batch `batch`) against one rank: the same
+    assignments, score bits and feasible counts for every pod, every rank the same truncation and rescue counts,
+    and the ranks' shards together conserving the requests (final state = initial - sum of the placed requests)."""
+    from ksched import Engine, MODE_BATCHED, cluster
+    cl = cluster.make_cluster("c4")
+    with Engine(mode=MODE_BATCHED, priority=cl.priority, domain=cl.domain, device=0, topk=16, batch=batch) as e:
+        e.load_nodes(cl.alloc_cpu, cl.alloc_mem, cl.alloc_pods)
+        oi, os_, of = e.schedule(cl.req_cpu, cl.req_mem, cl.req_pods)
+        one = e.stats()
+        fin1 = e.read_nodes()
+    assert one["pipeline"] == "persistent"
+    out = run_local(cl, world, calls=1, rings="uncached", batch=batch)
+    for r in range(world):
+        ri, rs, rf, pipe, nb, ntr, exr, nres = out[r][0][0]
+        assert pipe == "persistent"
+        bad = np.nonzero(ri != oi)[0][:5]
+        assert bad.size == 0, f"rank {r} of {world}: assignments differ from one rank at pods {bad}"
+        assert np.array_equal(rs, os_.view(np.int64)), f"rank {r}: score bits differ from one rank"
+        assert np.array_equal(rf, of), f"rank {r}: feasible counts differ from one rank"
+    st = [out[r][0][0] for r in range(world)]
+    assert len({x[5] for x in st}) == 1 and len({x[7] for x in st}) == 1, "ranks disagree on truncations / rescues"
+    got = [np.concatenate([out[r][1][k] for r in range(world)]) for k in range(3)]
+    placed = oi >= 0
+    for k, (a0, req) in enumerate(((cl.alloc_cpu, cl.req_cpu), (cl.alloc_mem, cl.req_mem), (cl.alloc_pods, None))):
+        d = np.zeros_like(a0)
+        np.add.at(d, oi[placed], 1 if req is None else req[placed])
+        assert np.array_equal(got[k], a0 - d), f"resource {k}: the shards do not conserve the placed requests"
+        assert np.array_equal(got[k], fin1[k]), f"resource {k}: the shards differ from one rank's final state"
+    print(f"c4 full size, {world} ranks at batch {batch}: {st[0][4]} batches, {st[0][5]} truncated, {st[0][7]} rescues "
+          f"(one rank: {one['batches']}, {one['truncations']}, {one['rescues']})")
+
+
+def test_xchg_full_c4_four_ranks(gpu_available):
+    """the sharded path through the whole c4 sequence, high-conflict stretch included."""
+    _full_c4_sharded(4, 64)
+
+
+def test_xchg_full_c4_eight_ranks(gpu_available):
+    _full_c4_sharded(8, 32)

@@ -215,3 +215,81 @@ def test_pass2_integer_threshold_is_a_superset():
     # L = 0 (fewer than KC bounds): every pair with a key passes, none without one (0xffff)
     t0 = int(screen_rec_threshold(F([0.0]))[0])
     assert 0x4900 <= t0 < 0xFFFF
+
+
+# ---- the non-fitting records (ksched_device.h screen_rec_nf / screen_rec_threshold_nf) -------------------------
+NF_BASE = F(3.375)  # kNfBase
+
+
+def screen_rec_nf(v):
+    """0x8000 | the f16 pattern of w = max(RN(kNfBase - v), 0) rounded down."""
+    v = np.asarray(v, np.float32)
+    with np.errstate(invalid="ignore"):
+        w = np.fmax(NF_BASE - v, F(0.0))
+    h = w.astype(np.float16)
+    hb = h.view(np.uint16).astype(np.int64)
+    return 0x8000 | (hb - (h.astype(np.float32) > w))
+
+
+def screen_rec_threshold_nf(L):
+    L = np.asarray(L, np.float32)
+    T = np.float64(NF_BASE) + 1.0 + np.float64(EPS) + 2.0 ** -20 - L.astype(np.float64)
+    h = T.astype(np.float32).astype(np.float16)
+    return np.where(T >= 0, h.view(np.uint16).astype(np.int64) + 1, -1)
+
+
+def needed(hb, tq, tqn):
+    """ksched_device.h screen_rec_needed"""
+    hb = np.asarray(hb, np.int64)
+    return np.where(hb & 0x8000, (hb & 0x7FFF) <= tqn, hb <= tq)
+
+
+def test_non_fitting_values_below_the_record_base():
+    """Every non-fitting screen value stays below kNfBase (at most two (1 - f) terms of (5/3))."""
+    rng = np.random.default_rng(21)
+    n = 400_000
+    r, a = _pairs(rng, n)
+    over = np.zeros((3, n), bool)
+    over[rng.integers(0, 3, n), np.arange(n)] = True
+    big = np.minimum(a + 1 + (rng.random((3, n)) * a).astype(np.int64), (1 << 52) - 1)
+    r = np.where(over & (a < (1 << 52) - 1), big, np.where(rng.random((3, n)) < 0.5, 0, r))  # zero requests: 1 - f = 1
+    v, _ = screen_pair(r[0], r[1], r[2], a[0], a[1], a[2])
+    nf = (r > a).any(axis=0)
+    assert nf.mean() > 0.9
+    assert np.nanmax(v[nf]) < NF_BASE and np.nanmax(v[nf]) > F(3.3)
+
+
+def test_non_fitting_record_is_an_upper_bound():
+    rng = np.random.default_rng(22)
+    v = np.concatenate([rng.uniform(0, 10 / 3, 2_000_000), 10 / 3 - rng.uniform(0, 0.3, 500_000) ** 2]).astype(np.float32)
+    h16 = np.arange(0, 0x42C0, dtype=np.uint16).view(np.float16).astype(np.float32)  # every f16 in [0, 3.375]
+    grid = NF_BASE - h16
+    v = np.concatenate([v, grid, np.nextafter(grid, F(0)), np.nextafter(grid, F(4)), F([0.0, 10 / 3, 3.3333337])])
+    v = v[(v >= 0) & (v < NF_BASE)]
+    hb = screen_rec_nf(v)
+    assert np.all(hb & 0x8000) and (hb & 0x7FFF).max() <= 0x42C0 and (hb & 0x7FFF).min() >= 0
+    ub = np.float64(NF_BASE) - rec_value(hb & 0x7FFF)
+    assert np.all(ub + 2.0 ** -21 >= v)
+    # tight where the late-c4 keys crowd (~3.25): within 2^-12 of v (the polynomial form there: 2^-8)
+    crowd = (v > F(3.2)) & (v < F(3.34))
+    assert np.all(ub[crowd] - v[crowd] < 2.0 ** -12)
+
+
+def test_pass2_two_form_threshold_is_a_superset():
+    """needed(): every record whose form's bound (+ 2^-21 + 1 + eps) reaches L passes, in both forms; the no-key
+    pattern 0xffff never does, an always-needed 0 always does."""
+    rng = np.random.default_rng(23)
+    L = np.concatenate([rng.uniform(0, 11.001, 60000), 4.25 - rng.uniform(0, 0.1, 20000), F([0.0, 1.0, 4.375, 11.0])]).astype(np.float32)
+    n = L.size
+    poly = rng.integers(0, 0x4901, n)
+    nfr = 0x8000 | rng.integers(0, 0x42C1, n)
+    tq, tqn = screen_rec_threshold(L), screen_rec_threshold_nf(L)
+    Ld = L.astype(np.float64)
+    need_p = (10.0 - rec_value(poly)) + 2.0 ** -21 + 1.0 + np.float64(EPS) >= Ld
+    need_n = (np.float64(NF_BASE) - rec_value(nfr & 0x7FFF)) + 2.0 ** -21 + 1.0 + np.float64(EPS) >= Ld
+    assert np.all(needed(poly, tq, tqn)[need_p])
+    assert np.all(needed(nfr, tq, tqn)[need_n])
+    assert not needed(np.full(n, 0xFFFF), tq, tqn).any()
+    assert needed(np.zeros(n, np.int64), tq, tqn)[Ld <= 11.0].all()
+    # an inactive lane (-1, -1) needs nothing
+    assert not needed(np.array([0, 0x8000, 0x4900, 0xFFFF]), -1, -1).any()
