@@ -1,17 +1,20 @@
 // anchor_ksched.go -- the cgo shim a maintainer drops into the reference's `anchor` package
 // (package main, next to anchor/schedule.go) to run predicate + priorities on libksched.
 //
-// It replaces, for the batch driver, the body of schedulePods (anchor/schedule.go:185-197) and, for
-// the watch path, schedulePod (anchor/schedule.go:68-89): the predicate / priorities evaluation of
-// every pod against every node (anchor/predicate.go:107-176, anchor/priorities.go:25-63) and the
+// It replaces the bodies of schedulePods (anchor/schedule.go:185-197, the reconcile loop's batch driver:
+// schedulePodsGPU below) and of schedulePod (anchor/schedule.go:68-89, what monitorUnscheduledPods calls for
+// every watched ADDED pod, anchor/schedule.go:47-66: schedulePodGPU below): the predicate / priorities
+// evaluation of every pod against every node (anchor/predicate.go:107-176, anchor/priorities.go:25-63) and the
 // "next pod sees the previous bind" accounting (usedResource, anchor/predicate.go:83-105) run on the
 // GPU; getNodes/getPods (anchor/tools.go:53-108), bind and postEvent (anchor/schedule.go:200-261,
-// anchor/tools.go:22-51) are the reference's own functions, called unchanged and in pod order.
+// anchor/tools.go:22-51) are the reference's own functions, called unchanged and in pod order.  The two call
+// sites change by one identifier each: schedulePods() -> schedulePodsGPU() in reconcileUnscheduledPods
+// (anchor/schedule.go:37) and schedulePod(&pod) -> schedulePodGPU(&pod) in monitorUnscheduledPods (:57).
 //
-// This file is not compiled in this repository's image (no Go toolchain); the same call sequence --
+// This file is not compiled in this repository's image (no Go toolchain); the same call sequences --
 // create, load_nodes, schedule, explain_pod per NO_FIT pod, ordered binds, apply_delta undo of a failed
-// bind -- is compiled and run against libksched.so as integration/ksched_driver.c by
-// tests/test_gpu_integration.py.  Type-checked by
+// bind, for a whole pending list and for one watched pod at a time -- are compiled and run against
+// libksched.so as integration/ksched_driver.c (batch and watch modes) by tests/test_gpu_integration.py.  Type-checked by
 // inspection against the reference: NodeList.Items is
 // []*Node (anchor/types.go:99), getUnscheduledPods returns []*Pod (anchor/schedule.go:145),
 // allocatableResource / bind take *Node (anchor/predicate.go:56, anchor/schedule.go:200),
@@ -175,6 +178,39 @@ func schedulePodsGPU() error {
 			break
 		}
 		start = resume
+	}
+	return nil
+}
+
+// schedulePodGPU is schedulePod (anchor/schedule.go:68-89) on the engine, for monitorUnscheduledPods
+// (anchor/schedule.go:47-66, which holds processorLock around the call).  predicate() re-reads the nodes and every
+// pod per call and recounts usedResource (anchor/predicate.go:107-115), so the cluster is loaded again here; then
+// the one pod is scheduled on the device (KSCHED_MODE_AUTO: the exact kernel for a single pod).  No node fits:
+// predicate()'s FailedScheduling event (failedSchedulingEvent, from ksched_explain_pod) and the reference's error.
+// A placement is bound with the reference's bind, unchanged; a failed bind returns its error, and the engine's
+// commit of the pod is undone so that its state is the API server's again.
+func schedulePodGPU(pod *Pod) error {
+	nodeList, err := getNodes()
+	errFatal(err, "failed to get nodes")
+	podList, err := getPods()
+	errFatal(err, "failed to get pods")
+	loadCluster(nodeList, podList)
+
+	r := requestedResource(pod) // anchor/predicate.go:69-81 (Pod = #containers)
+	rc, rm, rp := []int64{r.CPU}, []int64{r.Memory}, []int64{r.Pod}
+	var idx C.int32_t
+	kschedCheck(C.ksched_schedule(kctx, 1, i64p(rc), i64p(rm), i64p(rp), nil, &idx, nil, nil), "ksched_schedule")
+	switch idx {
+	case C.KSCHED_NO_FIT: // predicate() returned no node (anchor/schedule.go:74-76), after posting its event
+		failedSchedulingEvent(pod, 0, nodeList)
+		return fmt.Errorf("Unable to schedule pod (%s) failed to fit in any node", pod.Metadata.Name)
+	case C.KSCHED_NO_POSITIVE_SCORE: // the reference binds a nil node here and panics
+		return fmt.Errorf("no node scored > 0 for pod (%s)", pod.Metadata.Name)
+	}
+	if err := bind(pod, nodeList.Items[idx]); err != nil { // unchanged HTTP bind (anchor/schedule.go:200)
+		one := []int64{1}
+		kschedCheck(C.ksched_apply_delta(kctx, 1, &idx, i64p(rc), i64p(rm), i64p(one)), "ksched_apply_delta")
+		return err
 	}
 	return nil
 }

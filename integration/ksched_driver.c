@@ -18,8 +18,14 @@
  *          the program with KSCHED_E_UNKNOWN_NODE, as the reference's usedResource panics there
  *          (anchor/predicate.go:94-99)
  *
+ * Watch mode (argv[6] = "watch"): the shim's schedulePodGPU for monitorUnscheduledPods (anchor/schedule.go:47-89):
+ * the pending pods arrive one at a time, each is ONE ksched_schedule call of one pod, then explain_pod on NO_FIT
+ * or its bind; a failed bind undoes that pod's commit (ksched_apply_delta) and the next pod goes on from there --
+ * the same sequential semantics as the batch loop.  (The Go shim reloads the cluster per pod, as predicate()
+ * recounts per call; here the engine keeps the state the reloads would give.)
+ *
  * Input (argv[1]) and output (argv[2]) are flat little-endian files written / read by
- * tests/test_gpu_integration.py; argv[3..]: mode, topk, batch.  The "API server" is simulated: a bind
+ * tests/test_gpu_integration.py; argv[3..]: mode, topk, batch, "batch" | "watch".  The "API server" is simulated: a bind
  * of a pod listed in the input's fail set returns an error, every other bind succeeds.
  */
 #include <stdint.h>
@@ -85,7 +91,26 @@ int main(int argc, char **argv) {
     int64_t *counts = calloc((size_t)p * KSCHED_NUM_REASONS, 8);
     uint8_t *reason = malloc((size_t)(n > 0 ? n : 1));
     int64_t calls = 0, binds = 0, failed_binds = 0, undone = 0;
-    int64_t start = 0;
+    const int watch = argc > 6 && strcmp(argv[6], "watch") == 0;
+    for (int64_t i = 0; watch && i < p; ++i) {
+        /* schedulePodGPU(pending pod i) */
+        rcode = ksched_schedule(ctx, 1, rc + i, rm + i, rp + i, hdr[5] ? sel + i : NULL, idx + i, score + i, feas + i);
+        if (rcode != KSCHED_OK) die(ctx, "ksched_schedule", rcode);
+        ++calls;
+        if (idx[i] == KSCHED_NO_FIT) {
+            if ((rcode = ksched_explain_pod(ctx, 0, counts + i * KSCHED_NUM_REASONS, n > 0 ? reason : NULL)) != KSCHED_OK)
+                die(ctx, "ksched_explain_pod", rcode);
+            continue;
+        }
+        if (idx[i] < 0) continue;
+        if (!bind_fails[i]) { ++binds; continue; }
+        ++failed_binds;
+        const int64_t one = 1;
+        if ((rcode = ksched_apply_delta(ctx, 1, idx + i, rc + i, rm + i, &one)) != KSCHED_OK) die(ctx, "ksched_apply_delta", rcode);
+        ++undone;
+        idx[i] = BIND_FAILED;
+    }
+    int64_t start = watch ? p : 0;
     while (start < p) {
         const int64_t m = p - start;
         rcode = ksched_schedule(ctx, m, rc + start, rm + start, rp + start, hdr[5] ? sel + start : NULL, idx + start,

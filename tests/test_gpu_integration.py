@@ -135,3 +135,31 @@ def test_driver_watch_events(gpu_available, oracle_mod, tmp_path):
     r = subprocess.run([DRIVER, str(tmp_path / "in2.bin"), str(tmp_path / "out2.bin"), "1", "16", "64"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 6 and "unknown node" in r.stderr, (r.returncode, r.stderr)
+
+
+@pytest.mark.parametrize("case", ["c3", "best_price", "c5hc"])
+def test_driver_watch_path(gpu_available, oracle_mod, tmp_path, case):
+    """The shim's schedulePodGPU for monitorUnscheduledPods (anchor/schedule.go:47-89): one ksched_schedule call per
+    watched pod (KSCHED_MODE_AUTO: the exact kernel for one pod), explain_pod on NO_FIT, the bind, and a failed
+    bind's commit undone -- the same sequential semantics as the batch driver, pod by pod."""
+    from ksched import cluster
+    assert os.path.exists(DRIVER), "integration/ksched_driver not built (build() / make -C integration)"
+    if case == "c3":
+        cl = cluster.make_cluster("c3", n_nodes=3000, n_pods=400)
+    elif case == "c5hc":
+        cl = cluster.make_cluster("c5hc", n_nodes=2000, n_pods=400)
+    else:
+        cl = cluster.make_cluster("c2", n_nodes=800, n_pods=400)
+    rng = np.random.default_rng(9)
+    fails = np.sort(rng.choice(cl.n_pods, 5, replace=False))
+    write_input(tmp_path / "in.bin", cl, fails)
+    r = subprocess.run([DRIVER, str(tmp_path / "in.bin"), str(tmp_path / "out.bin"), "2", "16", "64", "watch"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    stats, idx, score, feas, counts, final = read_output(tmp_path / "out.bin", cl.n_nodes, cl.n_pods)
+    wi, ws, wf, wc, wst = expected(cl, fails, oracle_mod)
+    assert np.array_equal(idx, wi), "watch path: assignments differ"
+    assert np.array_equal(score.view(np.int64), ws.view(np.int64)) and np.array_equal(feas, wf)
+    assert np.array_equal(counts, wc), "watch path: FailedScheduling counts differ"
+    assert all(np.array_equal(a, b) for a, b in zip(final, wst)), "watch path: final state differs"
+    assert stats[0] == cl.n_pods and stats[2] == (wi == BIND_FAILED).sum()
