@@ -23,20 +23,8 @@
 
 #include <hip/hip_runtime.h>
 
-#ifndef KSCHED_RESCAN_UNROLL
-#define KSCHED_RESCAN_UNROLL 1  // the sequential path's touched-slot rescan with four loads in flight
-#endif
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0  // the exchange diagnostics of tests/diag/xchg_ring_experiment.py (a separate build)
-#endif
-#ifndef KSCHED_AB_NO_DRAIN
-#define KSCHED_AB_NO_DRAIN 0  // A/B builds only
-#endif
-#ifndef KSCHED_AB_S_FIRST
-#define KSCHED_AB_S_FIRST 0  // A/B builds only: the key matrix first in the commit's LDS (round 4's order)
-#endif
-#ifndef KSCHED_NO_TOUCH_SCREEN
-#define KSCHED_NO_TOUCH_SCREEN 0  // A/B builds: every touched-node key exact
 #endif
 
 #include "ksched_kernels.h"
@@ -361,7 +349,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
     constexpr int kSpcWaves = NT / 64;
     constexpr int kSpcThreads = NT;
     constexpr bool LAG3 = COH;  // the persistent pipeline runs at lag kPipeLag = 3
-    constexpr bool SCR = COH && PRIO != kPrioPrice && !KSCHED_NO_TOUCH_SCREEN;  // the touched-node screen (above)
+    constexpr bool SCR = COH && PRIO != kPrioPrice;  // the touched-node screen (above; KSCHED_NO_TOUCH_SCREEN=1 at run time)
     static_assert(!COH || kPipeLag == 3, "commit_spc_batch: the persistent pipeline's inheritance is lag 3");
     constexpr int kSpcRow = spc_slots<LAG3>() + 1;
     const int tid = threadIdx.x;
@@ -386,6 +374,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     L->plan[(A.batch + kPipeLag - 1) % kPlanRing] = ho.plan_next;
                     L->rseq = ho.rseq;
                     persist_plan(A, false, ho.cursor);
+                    st_coh(A.cursor_at, (uint64_t)ho.cursor);
                     drain_stores();  // every store of this commit lands before its hand-off record (below)
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
@@ -419,7 +408,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         // per-lane (or per-index) address register -- with S first, each of the arrays above it needed an address
         // register of its own, which the compiler hoisted out of the batch loop and spilled
         char *p = smem;
-        if (KSCHED_AB_S_FIRST) p += (size_t)64 * kSpcRow * sizeof(double);
         m.pbk = reinterpret_cast<double *>(p); p += (size_t)kSpcWaves * 64 * sizeof(double);
         m.pbx = reinterpret_cast<int64_t *>(p); p += (size_t)kSpcWaves * 64 * sizeof(int64_t);
         m.LK = reinterpret_cast<double *>(p); p += (size_t)K * 64 * sizeof(double);
@@ -439,7 +427,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
         m.ctl = reinterpret_cast<int32_t *>(p); p += 4 * sizeof(int32_t);
         m.thr = reinterpret_cast<float *>(p); p += 64 * sizeof(float);
         m.x2s = reinterpret_cast<int16_t *>(p); p += 64 * sizeof(int16_t);
-        m.S = KSCHED_AB_S_FIRST ? reinterpret_cast<double *>(smem) : reinterpret_cast<double *>(p);
+        m.S = reinterpret_cast<double *>(p);
         m.own = reinterpret_cast<int32_t *>(m.pbk);
         m.s0 = reinterpret_cast<int64_t *>(m.D);
         m.iy = reinterpret_cast<double *>(m.GS);
@@ -666,6 +654,7 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                     __hip_atomic_fetch_add(reinterpret_cast<unsigned long long *>(&A.ctl->stats[3]), 1ull,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     persist_plan(A, false, ho.cursor);
+                    st_coh(A.cursor_at, (uint64_t)ho.cursor);
                     drain_stores();  // every store of this commit lands before its hand-off record (below)
                     put_handoff(A.ctl, A.batch, 0, ho.cursor, ho.rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
                 }
@@ -1193,7 +1182,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                         rbk = up ? kv : rbk; rbi = up ? wi : rbi; rbs = up ? s : rbs;
                         if (__ballot(rescan)) {
                             if (rescan) {
-#if KSCHED_RESCAN_UNROLL
                                 // four slots' loads in flight, two running maxima (better() is a total order on
                                 // distinct nodes, so the fold order does not change the result)
                                 double k0 = -__builtin_inf(), k1 = -__builtin_inf();
@@ -1220,14 +1208,6 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
                                 }
                                 if (k1 != -__builtin_inf() && better(k1, i1, k0, i0)) { k0 = k1; i0 = i1; s0 = s1; }
                                 rbk = k0; rbi = i0; rbs = s0;
-#else
-                                rbk = -__builtin_inf(); rbi = kNoIdx; rbs = -1;
-                                for (int t = 0; t < nT; ++t) {
-                                    const double v = Srow[t];
-                                    const int32_t x = m.ti[t];
-                                    if (v != -__builtin_inf() && better(v, x, rbk, rbi)) { rbk = v; rbi = x; rbs = t; }
-                                }
-#endif
                             }
                         }
                     }
@@ -1312,11 +1292,12 @@ __device__ __forceinline__ int commit_spc_batch(const CommitArgs &A, char *smem,
             st_coh(&A.xout->count, (uint64_t)(uint32_t)base | (uint64_t)(uint32_t)A.batch << 32);  // {count, tag}
             L->cursor = p0 + done;
             persist_plan(A, done < nb, p0 + done);
+            st_coh(A.cursor_at, (uint64_t)L->cursor);  // (publish_committed<true> relies on this store and the drain)
             // every store of this commit -- the export, its {count, tag} header, the plan -- lands before the hand-off
             // record: commit(b + 1) may publish Ctl::committed = b + 2 before this workgroup publishes b + 1, and a
             // reader that sees b + 2 reads export(b) (round 5: without this drain a score workgroup could read the
             // header before it landed and skip a whole export)
-            if (!KSCHED_AB_NO_DRAIN) drain_stores();
+            drain_stores();
             if (A.xp) jitter_at(A.xp->jitter, A.batch, 101);
             put_handoff(A.ctl, A.batch, base, L->cursor, L->rseq, L->plan[(A.batch + kPipeLag) % kPlanRing]);
             if (A.trace_row) A.trace_row[53] = wall_clock64();  // the hand-off record issued

@@ -149,6 +149,8 @@ struct ksched_ctx {
     int64_t xring_bytes = 0, lring_bytes = 0;
     // exact workspace
     uint64_t *d_slots = nullptr;
+    int32_t *d_perm = nullptr;     // exact mode on one workgroup, best-price: nodes by (price asc, index asc)
+    int64_t perm_cap = 0;
     int32_t *d_err = nullptr;
     int64_t slots_cap = 0;
     // multi-GPU
@@ -206,7 +208,8 @@ struct ksched_ctx {
         bool no_pairs = false;   // KSCHED_NO_PAIRS: the screened scan's exact phase by rows (A/B of the pair lists)
         bool poison = false;     // KSCHED_POISON: workspace and LDS filled with 0xff before every persistent run
         int xchg_diag = 0;       // KSCHED_XCHG_DIAG (section 6.1's experiment): 1 ring zeroed by hipMemsetAsync, 2 local tags from 1
-        int64_t epoch_base = 0;  // KSCHED_XCHG_EPOCH_BASE (tests): a setup's granule tags start at least here (near 2^15: wrap)
+        int64_t epoch_base = 0;
+        int exact1_bs = 1024;    // KSCHED_EXACT1_BS (A/B): the one-workgroup exact kernel's block (1024, 512, 256)  // KSCHED_XCHG_EPOCH_BASE (tests): a setup's granule tags start at least here (near 2^15: wrap)
         bool plain_launch = false;  // KSCHED_PLAIN_LAUNCH: the persistent kernels without the cooperative launch API
                                     // (same residency check; profiled runs: DESIGN.md section 6.1)
         uint32_t jitter = 0;     // KSCHED_JITTER=<seed>: random delays at the persistent pipeline's protocol points
@@ -1053,6 +1056,32 @@ int enqueue_persistent(ksched_ctx *c) {
 int enqueue_exact(ksched_ctx *c) {
     if (c->o.nranks > 1) return fail(c, KSCHED_E_INVALID, "exact mode is single-GPU; use batched mode across ranks");
     const int64_t n = c->n_local;
+    // the whole node set in ONE workgroup's registers (k_exact1): no cross-workgroup exchange per pod
+    const bool price = c->o.priority == KSCHED_PRIORITY_BEST_PRICE;
+    const int max1 = price ? 16 : 4;
+    if (c->o.exact_wgs <= 1 && n > 0 && n <= (int64_t)kExact1Block * max1 && (!price || c->d_perm)) {
+        int bs = kExact1Block;
+        if (price && c->diag.exact1_bs == 512 && n <= 5120) bs = 512;
+        if (price && c->diag.exact1_bs == 256 && n <= 5120) bs = 256;
+        int npt = bs == 512 ? 10 : bs == 256 ? 20 : 1;
+        while ((int64_t)bs * npt < n) npt = npt < 4 ? npt + 1 : (npt < 6 && price ? npt + 1 : (npt < 8 ? 8 : (npt < 12 ? 12 : 16)));
+        HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
+        ExactArgs a{};
+        a.nodes = c->d_nodes; a.n = n; a.G = 1; a.per_wg = (int32_t)n;
+        a.pods = PodArgs{c->d_rc, c->d_rm, c->d_rp, c->d_sel, c->p};
+        a.out = OutArgs{c->d_oidx, c->d_osc, c->d_ofeas};
+        a.err = c->d_err;
+        a.perm = price ? c->d_perm : nullptr;
+        int e0 = -1;
+        HIPCHK(c, ev_begin(c, c->o.timing != 0, &e0, c->stream));
+        HIPCHK(c, launch_exact1(npt, bs, c->o.priority, c->o.domain, c->o.use_labels != 0, c->fast53, a, c->stream));
+        HIPCHK(c, ev_end(c, c->o.timing != 0, 0, e0, c->p * n, c->stream));
+        c->st.pair_evals = c->p * n;
+        c->st.batches = 0;
+        c->st.truncations = 0;
+        c->run_batches = 1;
+        return KSCHED_OK;
+    }
     int G = c->o.exact_wgs;
     int npt;
     if (G <= 0) {
@@ -1137,6 +1166,7 @@ int ksched_create(const ksched_opts *opts, ksched_ctx **out) {
     c->diag.plain_launch = env_int("KSCHED_PLAIN_LAUNCH", 0) != 0;
     c->diag.xchg_diag = env_int("KSCHED_XCHG_DIAG", 0);
     c->diag.epoch_base = env_int("KSCHED_XCHG_EPOCH_BASE", 0);
+    c->diag.exact1_bs = env_int("KSCHED_EXACT1_BS", 1024);
     c->diag.rescue_max = env_int("KSCHED_RESCUE_MAX", 4);
     c->diag.rescue_rate = env_int("KSCHED_RESCUE_RATE", 4);
     c->diag.rescue_look = env_int("KSCHED_RESCUE_LOOK", 0);
@@ -1190,7 +1220,7 @@ int ksched_destroy(ksched_ctx *c) {
     hipFree(c->d_nodes); hipFree(c->d_snap);
     hipFree(c->d_rc); hipFree(c->d_rm); hipFree(c->d_rp); hipFree(c->d_sel);
     hipFree(c->d_oidx); hipFree(c->d_osc); hipFree(c->d_ofeas);
-    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_dbg); hipFree(c->d_mdbg); hipFree(c->d_slots); hipFree(c->d_err);
+    hipFree(c->d_ws); hipFree(c->d_cursor); hipFree(c->d_dbg); hipFree(c->d_mdbg); hipFree(c->d_slots); hipFree(c->d_perm); hipFree(c->d_err);
     if (c->h_cursor) hipHostFree(c->h_cursor);
     for (hipEvent_t e : c->ev_pool) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1478,6 +1508,20 @@ int ksched_load_nodes(ksched_ctx *c, int64_t n, const int64_t *ac, const int64_t
     if (c->n_global < c->o.node_offset + n) return fail(c, KSCHED_E_INVALID, "load_nodes: nodes_global too small");
     c->has_labels = labels != nullptr;
     c->has_price = price != nullptr;
+    if (price && n > 0 && n <= (int64_t)kExact1Block * 16) {
+        // exact mode on one workgroup (k_exact1): the nodes in the best-price argmax's order -- price ascending,
+        // node index ascending on ties (prices are finite, -0 canonical: the order of price_key descending)
+        std::vector<int32_t> perm((size_t)n);
+        for (int64_t i = 0; i < n; ++i) perm[(size_t)i] = (int32_t)i;
+        std::stable_sort(perm.begin(), perm.end(), [&](int32_t x, int32_t y) { return h[(size_t)x].price < h[(size_t)y].price; });
+        HIPCHK(c, grow(&c->d_perm, &c->perm_cap, n, sizeof(int32_t)));
+        HIPCHK(c, hipMemcpyAsync(c->d_perm, perm.data(), (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    } else if (c->d_perm) {
+        hipFree(c->d_perm);
+        c->d_perm = nullptr;
+        c->perm_cap = 0;
+    }
     return KSCHED_OK;
 }
 

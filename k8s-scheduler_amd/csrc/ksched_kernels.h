@@ -12,9 +12,6 @@
 // are bit-identical to hipcc's f64 division for this path's operands.
 // See DESIGN.md for the correctness argument of the batched commit.
 #pragma once
-#ifndef KSCHED_AB_PUBLISH_STORE
-#define KSCHED_AB_PUBLISH_STORE 0  // A/B builds only
-#endif
 
 #include "ksched_device.h"
 
@@ -197,6 +194,7 @@ struct ExactArgs {
     uint64_t *slots;  // [2][G][4] granules {epoch:32 | value:32}; zeroed before every launch
     int32_t *err;     // device error word (1 = exchange timeout)
     int64_t timeout_ticks;
+    const int32_t *perm;  // k_exact1: slot -> node (best-price: nodes by price asc, index asc); null: slot = node
 };
 
 struct ScoreArgs {
@@ -314,17 +312,21 @@ __host__ __device__ inline size_t xdbg_commit_off(int64_t cap, int B, int R, int
 // on a cross-queue stream event (~12 us per hand-off).  Call from ONE wave that
 // made every global store of the commit (the others made none).
 // COH (persistent pipeline): every handed-off store was an sc1 store, so no L2 write-back is needed.
+// COH (persistent pipeline): the caller stored Ctl::cursor_at (store_cursor_at) before the drain in front of its
+// hand-off record, so every store a reader of Ctl::committed needs has landed: no store and no drain here (the
+// hand-off record itself is read only by the next commit, which polls it).
 template <bool COH = false>
 __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
-    if ((threadIdx.x & 63) == 0 && A.cursor_at)
-        st_coh(A.cursor_at, COH ? (uint64_t)A.loc->cursor : ld_coh(&A.ctl->cursor));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (!COH) {
+        if ((threadIdx.x & 63) == 0 && A.cursor_at) st_coh(A.cursor_at, ld_coh(&A.ctl->cursor));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if ((threadIdx.x & 63) == 0) {
         if (!COH || A.release) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        if (COH && !KSCHED_AB_PUBLISH_STORE)  // two commit workgroups: a maximum, so the count never steps back
+        if (COH)  // two commit workgroups: a maximum, so the count never steps back
             __hip_atomic_fetch_max(&A.ctl->committed, (unsigned long long)A.batch + 1ull, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         else
@@ -332,14 +334,9 @@ __device__ __forceinline__ void publish_committed(const CommitArgs &A) {
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     // persistent pipeline: the per-XCD replicas (lanes 0..7 of the publishing wave, one each)
-    if (COH && (threadIdx.x & 63) < kCtlReplicas) {
-        if (KSCHED_AB_PUBLISH_STORE)
-            __hip_atomic_store(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
+    if (COH && (threadIdx.x & 63) < kCtlReplicas)
+        __hip_atomic_fetch_max(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            __hip_atomic_fetch_max(&A.ctl->committed_x[threadIdx.x & 63].v, (unsigned long long)A.batch + 1ull,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 // every replica of Ctl::committed (the persistent pipeline's end and error paths; lanes 0..7)
 __device__ __forceinline__ void publish_committed_all(Ctl *ctl, unsigned long long v) {
@@ -663,6 +660,10 @@ hipError_t launch_selftest_div(int64_t n, const double *a, const double *b, doub
                                hipStream_t s);
 
 constexpr int kExactBlock = 256;
+constexpr int kExact1Block = 1024;  // k_exact1: the whole node set in one workgroup
+// exact mode on one workgroup of bs threads, npt node slots each: bs 1024 with npt 1-4 (resource) or 1-6, 8, 12, 16
+// (best-price); best-price also (512, 10) and (256, 20)
+hipError_t launch_exact1(int npt, int bs, int prio, int dom, bool lab, bool f53, const ExactArgs &a, hipStream_t s);
 
 // score kernel geometry: 4 waves per workgroup, 2 workgroups per CU at the default grid
 constexpr int kScoreWaves = 8;

@@ -198,6 +198,149 @@ __global__ __launch_bounds__(kExactBlock) void k_exact(ExactArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Exact mode on ONE workgroup (kExact1Block threads; n <= kExact1Block * NPT): every node lives in a register
+// slot of this workgroup, so a pod is decided with one workgroup barrier and no cross-workgroup exchange (k_exact
+// with G > 1 pays a round of tagged granules through L2 per pod, ~2.7 us on c2).  Thread t holds slots
+// s = t + k * kExact1Block.
+//   best-price: slot s is the node of rank s in (price asc, node index asc) -- the order of the reference's
+//     argmax over -price with the lowest index on ties (README.md:37-64; price_key) -- so a pod's node is the
+//     FIRST feasible slot: per wave one ballot per k (its lowest set bit), the minimum over the waves; the feasible
+//     count is the sum of the ballots' popcounts.  No key is compared at all.
+//   resource: slot s is node s; per pod every lane keys its slots, wave arg-best, the waves' bests through LDS.
+// Restated by the same oracle as k_exact (oracle/cpu_ref.c or_schedule); results bit-identical.
+// ------------------------------------------------------------------------------------------------
+template <int NPT, int BS, int PRIO, int DOM, bool LAB, bool F53>
+__global__ __launch_bounds__(BS) void k_exact1(ExactArgs A) {
+    constexpr int kExact1Block = BS;
+    constexpr int W = kExact1Block / 64;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const double y3 = recip(3.0);
+    constexpr bool kRes = PRIO != kPrioPrice;
+    int64_t a0[NPT], a1[NPT], a2[NPT];
+    double f0[kRes ? NPT : 1], f1[kRes ? NPT : 1], f2[kRes ? NPT : 1];
+    double yy0[kRes ? NPT : 1], yy1[kRes ? NPT : 1], yy2[kRes ? NPT : 1];
+    uint64_t lab[NPT];
+    float pr[NPT];
+    int32_t id[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+        const int64_t sl = tid + (int64_t)k * kExact1Block;
+        id[k] = kNoIdx;
+        a0[k] = a1[k] = a2[k] = 0; lab[k] = 0; pr[k] = 0.f;
+        if constexpr (kRes) { f0[k] = f1[k] = f2[k] = 0.0; yy0[k] = yy1[k] = yy2[k] = 0.0; }
+        if (sl < A.n) {
+            const int32_t j = A.perm ? A.perm[sl] : (int32_t)sl;
+            const NodeRec &nd = A.nodes[j];
+            a0[k] = nd.a[0]; a1[k] = nd.a[1]; a2[k] = nd.a[2];
+            lab[k] = nd.labels; pr[k] = nd.price; id[k] = j;
+            if constexpr (kRes) {
+                f0[k] = nd.af[0]; f1[k] = nd.af[1]; f2[k] = nd.af[2];
+                yy0[k] = nd.y[0]; yy1[k] = nd.y[1]; yy2[k] = nd.y[2];
+            }
+        }
+    }
+    __shared__ int32_t s_cnt[2][W];
+    __shared__ int32_t s_slot[2][W];  // best-price: the wave's first feasible slot (INT32_MAX: none)
+    __shared__ double s_key[2][W];    // resource: the wave's best (key, node)
+    __shared__ int32_t s_idx[2][W];
+    // the next pod's request is loaded one pod ahead: its latency hides behind the current pod
+    int64_t nrc = 0, nrm = 0, nrp = 0;
+    uint64_t nsel = 0;
+    if (A.pods.p > 0) { nrc = A.pods.rc[0]; nrm = A.pods.rm[0]; nrp = A.pods.rp[0]; nsel = LAB ? A.pods.sel[0] : 0; }
+    for (int64_t i = 0; i < A.pods.p; ++i) {
+        const int par = (int)(i & 1);
+        const int64_t rc = nrc, rm = nrm, rp = nrp;
+        const uint64_t sel = nsel;
+        if (i + 1 < A.pods.p) {
+            nrc = A.pods.rc[i + 1]; nrm = A.pods.rm[i + 1]; nrp = A.pods.rp[i + 1];
+            nsel = LAB ? A.pods.sel[i + 1] : 0;
+        }
+        int32_t cnt = 0;
+        int32_t oidx = -1;
+        double osc = 0.0;
+        if constexpr (!kRes) {
+            int32_t first = 0x7fffffff;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                const bool f = id[k] != kNoIdx && fits(rc, rm, rp, sel, a0[k], a1[k], a2[k], lab[k], LAB);
+                const uint64_t m = __ballot(f);
+                cnt += __popcll(m);
+                if (first == 0x7fffffff && m) first = k * kExact1Block + wave * 64 + (int)__builtin_ctzll(m);
+            }
+            if (lane == 0) { s_slot[par][wave] = first; s_cnt[par][wave] = cnt; }
+            __syncthreads();
+            int32_t gs = s_slot[par][0], gc = s_cnt[par][0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) { gs = s_slot[par][w] < gs ? s_slot[par][w] : gs; gc += s_cnt[par][w]; }
+            // the first feasible slot's owner commits it and writes the pod's results; no feasible node: thread 0
+            if (gc == 0) {
+                if (tid == 0) { A.out.idx[i] = -1; A.out.score[i] = 0.0; A.out.feas[i] = 0; }  // NO_FIT
+            } else if ((gs & (kExact1Block - 1)) == tid) {
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    if (gs == k * kExact1Block + tid) {  // commit: used += request, ONE pod (anchor/predicate.go:99-102)
+                        A.out.idx[i] = id[k];
+                        A.out.score[i] = 0.0 - price_key(pr[k]);
+                        A.out.feas[i] = gc;
+                        a0[k] = wsub(a0[k], rc); a1[k] = wsub(a1[k], rm); a2[k] = wsub(a2[k], 1);
+                    }
+                }
+            }
+            (void)oidx; (void)osc;
+        } else {
+            const double rcf = (double)rc, rmf = (double)rm, rpf = (double)rp;
+            double bk = -__builtin_inf();
+            int32_t bi = kNoIdx;
+#pragma unroll
+            for (int k = 0; k < NPT; ++k) {
+                if (id[k] != kNoIdx) {
+                    const bool f = fits(rc, rm, rp, sel, a0[k], a1[k], a2[k], lab[k], LAB);
+                    cnt += f;
+                    double key;
+                    if (pair_key_fast<PRIO, DOM, F53>(f, rc, rm, rp, rcf, rmf, rpf, a0[k], a1[k], a2[k], f0[k], f1[k],
+                                                      f2[k], yy0[k], yy1[k], yy2[k], y3, pr[k], &key) &&
+                        better(key, id[k], bk, bi)) {
+                        bk = key;
+                        bi = id[k];
+                    }
+                }
+            }
+            int32_t aux = 0;
+            wave_argbest(bk, bi, aux);
+            cnt = (int32_t)wave_sum_i64(cnt);
+            if (lane == 0) { s_key[par][wave] = bk; s_idx[par][wave] = bi; s_cnt[par][wave] = cnt; }
+            __syncthreads();
+            double gk = s_key[par][0];
+            int32_t gi = s_idx[par][0], gc = s_cnt[par][0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) {
+                gc += s_cnt[par][w];
+                if (better(s_key[par][w], s_idx[par][w], gk, gi)) { gk = s_key[par][w]; gi = s_idx[par][w]; }
+            }
+            oidx = gc == 0 ? -1 : (gi == kNoIdx ? -2 : gi);  // NO_FIT / NO_POSITIVE_SCORE (anchor/schedule.go:74-76)
+            osc = oidx >= 0 ? gk : 0.0;
+            if (oidx >= 0) {
+#pragma unroll
+                for (int k = 0; k < NPT; ++k) {
+                    if (id[k] == gi) {
+                        a0[k] = wsub(a0[k], rc); a1[k] = wsub(a1[k], rm); a2[k] = wsub(a2[k], 1);
+                        f0[k] = (double)a0[k]; f1[k] = (double)a1[k]; f2[k] = (double)a2[k];
+                        yy0[k] = recip_or_zero(a0[k], f0[k]); yy1[k] = recip_or_zero(a1[k], f1[k]);
+                        yy2[k] = recip_or_zero(a2[k], f2[k]);
+                    }
+                }
+            }
+            if (tid == 0) { A.out.idx[i] = oidx; A.out.score[i] = osc; A.out.feas[i] = gc; }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+        if (id[k] != kNoIdx) set_node(A.nodes + id[k], a0[k], a1[k], a2[k]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Batched mode, stage 1: fused predicate + score + top-KC per (pod, workgroup).  Lane = pod of the
 // batch.  A workgroup is kScoreWaves waves; wave w of workgroup g scans sub-chunk s = g + G*w of the
 // NSC = G*kScoreWaves sub-chunks, i.e. the nodes j with j mod NSC == s: workgroup g holds the nodes
@@ -937,6 +1080,41 @@ hipError_t exact_npt(int npt, const ExactArgs &a, int block, bool coop, hipStrea
     }
 }
 
+template <int NPT, int BS, int PRIO, int DOM, bool LAB, bool F53>
+hipError_t exact1_one(const ExactArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((k_exact1<NPT, BS, PRIO, DOM, LAB, F53>), dim3(1), dim3(BS), 0, s, a);
+    return hipGetLastError();
+}
+// (npt, block): resource slots <= 4 per thread of 1024 (registers); best-price more
+template <int PRIO, int DOM, bool LAB, bool F53>
+hipError_t exact1_npt(int npt, int bs, const ExactArgs &a, hipStream_t s) {
+    if (bs == 1024) {
+        switch (npt) {
+            case 1: return exact1_one<1, 1024, PRIO, DOM, LAB, F53>(a, s);
+            case 2: return exact1_one<2, 1024, PRIO, DOM, LAB, F53>(a, s);
+            case 3: return exact1_one<3, 1024, PRIO, DOM, LAB, F53>(a, s);
+            case 4: return exact1_one<4, 1024, PRIO, DOM, LAB, F53>(a, s);
+            default: break;
+        }
+        if constexpr (PRIO == kPrioPrice) {
+            switch (npt) {
+                case 5: return exact1_one<5, 1024, PRIO, DOM, LAB, F53>(a, s);
+                case 6: return exact1_one<6, 1024, PRIO, DOM, LAB, F53>(a, s);
+                case 8: return exact1_one<8, 1024, PRIO, DOM, LAB, F53>(a, s);
+                case 12: return exact1_one<12, 1024, PRIO, DOM, LAB, F53>(a, s);
+                case 16: return exact1_one<16, 1024, PRIO, DOM, LAB, F53>(a, s);
+                default: return hipErrorInvalidValue;
+            }
+        }
+        return hipErrorInvalidValue;
+    }
+    if constexpr (PRIO == kPrioPrice) {
+        if (bs == 512 && npt == 10) return exact1_one<10, 512, PRIO, DOM, LAB, F53>(a, s);
+        if (bs == 256 && npt == 20) return exact1_one<20, 256, PRIO, DOM, LAB, F53>(a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
 template <int KC, int PRIO, int DOM, bool LAB, bool F53>
 hipError_t score_one(const ScoreArgs &a, int pod_groups, hipStream_t s) {
     const size_t lds = score_lds_bytes(KC);
@@ -1075,6 +1253,10 @@ hipError_t launch_prep_nodes(NodeRec *nodes, int64_t n, hipStream_t s) {
 hipError_t launch_exact(int npt, int prio, int dom, bool lab, bool f53, const ExactArgs &a, int block, bool coop,
                         hipStream_t s) {
     KSCHED_DISPATCH(prio, dom, lab, f53, (exact_npt<P_, D_, L_, F_>(npt, a, block, coop, s)));
+}
+
+hipError_t launch_exact1(int npt, int bs, int prio, int dom, bool lab, bool f53, const ExactArgs &a, hipStream_t s) {
+    KSCHED_DISPATCH(prio, dom, lab, f53, (exact1_npt<P_, D_, L_, F_>(npt, bs, a, s)));
 }
 
 hipError_t launch_score_topk(int KC, int prio, int dom, bool lab, bool f53, const ScoreArgs &a, int pod_groups,

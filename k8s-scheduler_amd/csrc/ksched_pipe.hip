@@ -47,10 +47,7 @@ constexpr int kPU = 4;                 // rows per score step (independent key c
 #ifndef KSCHED_XCHG_DEBUG
 #define KSCHED_XCHG_DEBUG 0
 #endif
-#ifndef KSCHED_SCREEN_PU
-#define KSCHED_SCREEN_PU 4
-#endif
-constexpr int kSPU = KSCHED_SCREEN_PU;  // rows per step of the screened scan's passes
+constexpr int kSPU = 4;  // rows per step of the screened scan's passes
 // The screened scan's exact phase over (row, pod) pairs: each pod's needed rows (at most kPairCap; ~4-8 on c4) and
 // the batch's pairs (at most kPairMax) -- past either the batch takes the row path (every needed row for every pod)
 constexpr int kPairCap = 48;
@@ -202,15 +199,9 @@ __device__ __forceinline__ void set_row(NodeRec *nd, int64_t a0, int64_t a1, int
 // DISTINCT rows, so the KC-th largest of them is at most the KC-th largest key of the workgroup -- a valid
 // L, at most slightly weaker than the KC-th largest of all the rows' bounds (tests/diag/screen_sim.py: c4 exact
 // rows +4 %).  Otherwise a sorted top-KC insertion.
-#ifndef KSCHED_SCORE_PREFETCH
-#define KSCHED_SCORE_PREFETCH 1
-#endif
-#ifndef KSCHED_SLOT_BOUND
-#define KSCHED_SLOT_BOUND 1
-#endif
 template <int KC, int SPU>
 __device__ __forceinline__ void bound_slots(uint32_t (&t)[KC], const uint32_t (&xs)[SPU]) {
-    if constexpr (KSCHED_SLOT_BOUND && SPU % KC == 0) {
+    if constexpr (SPU % KC == 0) {
 #pragma unroll
         for (int u = 0; u < SPU; ++u) t[u % KC] = t[u % KC] > xs[u] ? t[u % KC] : xs[u];
     } else {
@@ -419,7 +410,7 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
     constexpr bool kPairs = kScreen;
     const bool pairs_ok = kPairs && !P.no_pairs && ScoreLayout<KC, K>::pairs_fit(R);
     constexpr int kScreenOffBatches = 16;
-    constexpr bool kPrefetch = kSW > 8 && KSCHED_SCORE_PREFETCH;  // wave kSW - 1 does not fold
+    constexpr bool kPrefetch = kSW > 8;  // wave kSW - 1 does not fold
     int64_t scr_off_until = 0;  // wave 0: batches before this one scan unscreened
     int64_t ex_rows = 0, scan_rows = 0;  // tid 0: rows scored exactly / rows scanned (progress words 4, 5)
     const int64_t Rvalid = (n - g + G - 1) / G;  // rows of this workgroup that hold a node
@@ -1618,18 +1609,14 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
         __syncthreads();
     }
     if (blk < kCommitWGs) {
-#ifndef KSCHED_PROBE_NO_COMMIT
         commit_role<K, PRIO, DOM, LAB, F53>(P, smem, blk);
-#endif
         return;
     }
     if (blk < kCommitWGs + P.G) {
         PipeCtl *pc = reinterpret_cast<PipeCtl *>(smem);
         if (threadIdx.x == 0) { pc->sbar = 0; pc->mbar = 0; }
         __syncthreads();
-#ifndef KSCHED_PROBE_NO_SCORE
         score_role<KC, K, PRIO, DOM, LAB, F53>(P, smem, blk - kCommitWGs);
-#endif
         return;
     }
     // a merger workgroup: kMS independent pod slots of kMT threads
@@ -1638,9 +1625,7 @@ __global__ __launch_bounds__(kPipeThreads) void k_pipe(PipeLaunch L) {
     char *sbase = smem + (size_t)slot * MergeLayout<KC, K>::slot_bytes;
     if (threadIdx.x % kMT == 0) reinterpret_cast<MergeCtl *>(sbase)->mbar = 0;
     __syncthreads();  // the only workgroup-wide barrier: before the slots part
-#ifndef KSCHED_PROBE_NO_MERGE
     if (id < P.B) merge_role<KC, K, PRIO, DOM, LAB, F53>(P, sbase, id);
-#endif
 }
 
 template <int KC, int K, int PRIO, int DOM, bool LAB, bool F53>

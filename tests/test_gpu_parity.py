@@ -140,6 +140,38 @@ def test_exact_mode_workgroup_counts(gpu_available, oracle_mod):
         assert_same(run_engine(cl, MODE_EXACT, exact_wgs=g), want, f"G={g}")
 
 
+@pytest.mark.parametrize("case", ["c2", "c2_16k", "c3_4k", "c5_3k", "edge_res", "edge_price", "ties_price"])
+def test_exact_one_workgroup(gpu_available, oracle_mod, case):
+    """Exact mode on ONE workgroup (k_exact1: every node in a register slot of one 1024-thread workgroup, one
+    barrier per pod; best-price as the first feasible node in (price, index) order): bit-exact against the oracle,
+    and equal to the multi-workgroup exchange kernel where that one fits."""
+    from ksched import MODE_EXACT, cluster
+    if case == "c2":
+        cl = cluster.make_cluster("c2", n_pods=2000)
+    elif case == "c2_16k":
+        cl = cluster.make_cluster("c2", n_nodes=16000, n_pods=600)
+    elif case == "c3_4k":
+        cl = cluster.make_cluster("c3", n_nodes=4000, n_pods=800)
+    elif case == "c5_3k":
+        cl = cluster.make_cluster("c5", n_nodes=3000, n_pods=800)
+    elif case == "edge_res":
+        cl = cluster.random_small(31, n_nodes=900, n_pods=700)
+    elif case == "edge_price":
+        cl = cluster.random_small(32, n_nodes=900, n_pods=700, priority=cluster.PRIORITY_BEST_PRICE,
+                                  domain=cluster.DOMAIN_FEASIBLE, use_labels=True)
+    else:  # every node the same price: the lowest index wins each time
+        cl = cluster.make_cluster("c2", n_nodes=3000, n_pods=900)
+        cl.price = np.full(cl.n_nodes, 0.5, np.float32)
+        cl.price[::7] = -0.0  # "-0" is "0": ties with the zero-priced nodes by index
+        cl.price[::11] = 0.0
+    want = oracle_mod.schedule(cl, nthreads=8)
+    got = run_engine(cl, MODE_EXACT)
+    assert_same(got, want, f"{case} one workgroup")
+    assert got[4]["pipeline"] == "exact"
+    if cl.n_nodes <= 2 * 256 * 8:
+        assert_same(run_engine(cl, MODE_EXACT, exact_wgs=2), want, f"{case} two workgroups")
+
+
 def test_apply_delta_and_state_roundtrip(gpu_available, oracle_mod):
     from ksched import Engine, MODE_EXACT, cluster
     cl = cluster.make_cluster("c3", n_nodes=2000, n_pods=300)

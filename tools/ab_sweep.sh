@@ -1,7 +1,7 @@
 #!/bin/bash
 # Same-box A/B of in-tree builds over several workloads (tools/sweep.py specs), alternated twice.
 #   AB_VARIANTS="main norescan" AB_SPECS="c4:batched:16:64 c5hc:batched:16:64" bash tools/ab_sweep.sh
-# (main = the tree's libksched.so; any other name = k8s-scheduler_amd/libksched_<name>.so, tools/build_variant.sh)
+# (main = the tree's libksched.so; any other name = k8s-scheduler_amd/libksched_<name>.so, tools/build_base.sh)
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 V=${AB_VARIANTS:-"main base"}
