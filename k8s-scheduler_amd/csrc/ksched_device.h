@@ -288,6 +288,36 @@ __device__ __forceinline__ float screen_q(float c, float m, float p, bool okc, b
     return v;
 }
 
+// Pass 1's screen of one pair from its f32 fractions (c, m, p), in a VALU-only form (no per-resource predicate
+// masks, whose combination costs scalar-unit instructions shared by the workgroup's 12 waves):
+//   amb: some fraction within 2^-20 of 1, or NaN -- the int64 compares decide such a pair.  |f - 1| is exact near 1
+//        (Sterbenz) and >= 0.5 elsewhere, so |f - 1| > 2^-20 is exactly screen_q's (f < kFracLo || f > kFracHi); the
+//        min of the three carries a NaN through 0 * S (min itself drops NaN operands);
+//   rf:  every resource fits -- for a non-ambiguous pair, the largest fraction mx below 1;
+//   v:   rf ? 10 - (5/3)(S + Q) + (5/9) S^2 : (5/3) * sum_k sat(1 - f_k), sat(x) = clamp(x, 0, 1): a non-fitting
+//        resource's f > 1 (not ambiguous) clamps to 0, a fitting one's 1 - f is in (0, 1].  Fused multiply-adds in the
+//        polynomial (Q, and its two combinations), so its rounding error is at most screen_q's bound (< 1.3e-5;
+//        tests/test_screen_bound.py emulates this form too).
+struct ScreenV {
+    float v, mx;
+    bool amb, rf;
+};
+__device__ __forceinline__ float sat01(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 1.0f); }
+__device__ __forceinline__ ScreenV screen_fast(float c, float m, float p) {
+    ScreenV o;
+    const float S = (c + m) + p;
+    o.mx = __builtin_fmaxf(__builtin_fmaxf(c, m), p);
+    const float d = __builtin_fminf(__builtin_fminf(__builtin_fabsf(c - 1.0f), __builtin_fabsf(m - 1.0f)),
+                                    __builtin_fabsf(p - 1.0f));
+    o.amb = !(__builtin_fmaf(0.0f, S, d) > 0x1p-20f);
+    o.rf = o.mx < 1.0f;
+    const float Q = __builtin_fmaf(c, c, __builtin_fmaf(m, m, p * p));
+    const float poly = __builtin_fmaf(5.0f / 9.0f, S * S, __builtin_fmaf(-5.0f / 3.0f, S + Q, 10.0f));
+    const float nf = (5.0f / 3.0f) * ((sat01(1.0f - c) + sat01(1.0f - m)) + sat01(1.0f - p));
+    o.v = o.rf ? poly : nf;
+    return o;
+}
+
 // The screened scan's per-pair record (pass 1 -> pass 2): a 16-bit upper bound of a screen value v (NaN allowed),
 // in two forms by the pair's screen form (screen_q's rf):
 //   resource-fitting (polynomial, v <= 10): the f16 bit pattern h of w = RN(10 - v) rounded DOWN (round toward

@@ -607,18 +607,18 @@ __device__ __forceinline__ void score_role(const PersistArgs &P, char *smem, con
                     for (int u = 0; u < kSPU; ++u) {
                         const int r = r0 + u * kSW;
                         const bool valid = r < Rv;
-                        const float c = qc * yv[u].x, m = qm * yv[u].y, p = qp * yv[u].z;
-                        const bool okc = c < kFracLo, okm = m < kFracLo, okp = p < kFracLo;
-                        const bool amb = !(okc || c > kFracHi) || !(okm || m > kFracHi) || !(okp || p > kFracHi);
-                        const bool f = okc & okm & okp & (!LAB || (lb[u] & sel) == sel);
+                        const ScreenV sv = screen_fast(qc * yv[u].x, qm * yv[u].y, qp * yv[u].z);
+                        const float v = sv.v;
+                        const bool amb = sv.amb, rf = sv.rf;
+                        const bool f = rf && (!LAB || (lb[u] & sel) == sel);
                         const bool el = DOM == kDomAll || f;
-                        bool lo_ok;
-                        const float v = screen_q(c, m, p, okc, okm, okp, &lo_ok);
+                        // a lower bound only where the key is surely there: a resource-fitting pair whose largest fraction
+                        // is below 0.999 (its balanced part cannot vanish), or a non-fitting one; and v > eps
+                        const bool lo_ok = !(rf && sv.mx >= 0.999f) && v > kScreenEps;
                         cnt += (valid && f && !amb) ? 1 : 0;
                         xs[u] = (valid && active && el && lo_ok && !amb) ? __float_as_uint(v + (1.0f - kScreenEps)) : 0u;
                         // the pair's upper bound (screen_rec / screen_rec_nf by the screen's form): 0 (always needed)
                         // when ambiguous, 0xffff (never needed) without a key
-                        const bool rf = okc & okm & okp;
                         ww[u] = __builtin_fmaxf((rf ? 10.0f : kNfBase) - v, 0.0f);
                         nrm[u] = (!amb && el) ? (rf ? 1u : 0x8001u) : 0u;
                         hh[u] = amb ? 0u : 0xffffu;

@@ -293,3 +293,82 @@ def test_pass2_two_form_threshold_is_a_superset():
     assert needed(np.zeros(n, np.int64), tq, tqn)[Ld <= 11.0].all()
     # an inactive lane (-1, -1) needs nothing
     assert not needed(np.array([0, 0x8000, 0x4900, 0xFFFF]), -1, -1).any()
+
+
+# ---- pass 1's VALU form (ksched_device.h screen_fast) ------------------------------------------------------------
+def fma32(a, b, c):
+    """f32 fused multiply-add: a * b + c rounded once (the product is exact in long double, the sum to 64 bits)"""
+    L = np.longdouble
+    return (np.asarray(a, np.float32).astype(L) * np.asarray(b, np.float32).astype(L) + np.asarray(c, np.float32).astype(L)).astype(np.float32)
+
+
+def screen_fast(rc, rm, rp, ac, am, ap):
+    """(v, mx, amb, rf) as screen_fast computes them from pass 1's f32 fractions."""
+    rc, rm, rp, ac, am, ap = (np.asarray(x, np.int64) for x in (rc, rm, rp, ac, am, ap))
+    with np.errstate(all="ignore"):
+        c, m, p = screen_req(rc) * screen_recip(ac), screen_req(rm) * screen_recip(am), screen_req(rp) * screen_recip(ap)
+        S = (c + m) + p
+        mx = np.fmax(np.fmax(c, m), p)
+        d = np.fmin(np.fmin(np.abs(c - F(1)), np.abs(m - F(1))), np.abs(p - F(1)))
+        amb = ~(fma32(F(0), S, d) > F(2.0 ** -20))
+        rf = mx < F(1)
+        Q = fma32(c, c, fma32(m, m, p * p))
+        poly = fma32(F(5.0 / 9.0), S * S, fma32(F(-5.0 / 3.0), S + Q, F(10)))
+        sat = lambda x: np.clip(x, F(0), F(1))  # noqa: E731
+        nf = F(5.0 / 3.0) * ((sat(F(1) - c) + sat(F(1) - m)) + sat(F(1) - p))
+        v = np.where(rf, poly, nf).astype(np.float32)
+    return v, mx, amb, rf
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_screen_fast_matches_the_bounds(seed):
+    """screen_fast: the same ambiguity and fit classes as screen_q's compares, and the same error bounds: the
+    polynomial within BOUND of the f64 score (lower-bound use where mx < 0.999), the non-fitting form within BOUND_NF
+    and below kNfBase."""
+    rng = np.random.default_rng(seed)
+    n = 300_000
+    r, a = _pairs(rng, n)
+    over = rng.random((3, n)) < 0.25
+    big = np.minimum(a + 1 + (rng.random((3, n)) * a * 3).astype(np.int64), (1 << 52) - 1)
+    r = np.where(over & (a < (1 << 52) - 1), big, r)
+    near = rng.random(n) < 0.05                                   # fractions within a few ulps of 1
+    k = rng.integers(0, 3, n)
+    r[k[near], np.nonzero(near)[0]] = a[k[near], np.nonzero(near)[0]] + rng.integers(-2, 3, near.sum())
+    r = np.maximum(r, 0)
+    v, mx, amb, rf = screen_fast(r[0], r[1], r[2], a[0], a[1], a[2])
+    qc, qm, qp = screen_req(r[0]), screen_req(r[1]), screen_req(r[2])
+    with np.errstate(all="ignore"):
+        c, m, p = qc * screen_recip(a[0]), qm * screen_recip(a[1]), qp * screen_recip(a[2])
+        lo, hi = F(1) - F(2.0 ** -20), F(1) + F(2.0 ** -20)
+        amb_q = ~((c < lo) | (c > hi)) | ~((m < lo) | (m > hi)) | ~((p < lo) | (p > hi))
+    assert np.array_equal(amb, amb_q), "ambiguity classes differ from screen_q's compares"
+    ok = ~amb
+    assert np.array_equal(rf[ok], ((c < lo) & (m < lo) & (p < lo))[ok])
+    s64 = exact_score(r[0], r[1], r[2], a[0], a[1], a[2])
+    pf = ok & rf & (mx < F(0.999))
+    err = np.abs(v[pf].astype(np.float64) - s64[pf])
+    assert err.max() < BOUND, f"polynomial: worst error {err.max():.3e}"
+    upf = ok & rf                                             # every resource-fitting pair: an upper bound
+    assert np.all(v[upf].astype(np.float64) + float(EPS) >= s64[upf])
+    nfm = ok & ~rf
+    assert nfm.mean() > 0.2
+    err = np.abs(v[nfm].astype(np.float64) - s64[nfm])
+    assert err.max() < BOUND_NF, f"non-fitting: worst error {err.max():.3e}"
+    assert v[nfm].max() < NF_BASE
+    # the pass-1 lower bound (lo_ok) only of eligible keys
+    lo_ok = ok & ~(rf & (mx >= F(0.999))) & (v > EPS)
+    assert np.all((v[lo_ok] - EPS).astype(np.float64) < s64[lo_ok]) and np.all(s64[lo_ok] > 0)
+
+
+def test_screen_fast_nan_is_ambiguous():
+    """An unscreenable operand (negative or >= 2^52 request, zero or negative allocatable) makes a fraction NaN: the
+    pair is ambiguous whichever resource it is (the min of the |f - 1| drops NaN; 0 * S carries it)."""
+    for k in range(3):
+        r = np.array([[10], [10], [1]], np.int64)
+        a = np.array([[100], [100], [10]], np.int64)
+        a[k, 0] = 0
+        v, mx, amb, rf = screen_fast(r[0], r[1], r[2], a[0], a[1], a[2])
+        assert amb[0], k
+        r2 = r.copy(); a2 = np.array([[100], [100], [10]], np.int64)
+        r2[k, 0] = -3
+        assert screen_fast(r2[0], r2[1], r2[2], a2[0], a2[1], a2[2])[2][0], k
