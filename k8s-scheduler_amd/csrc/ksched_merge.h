@@ -253,11 +253,9 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b, 
 // with ONE barrier and no LDS-latency-bound loops: every rank is counted over register broadcasts
 // (v_readlane of all 64 lanes) instead of LDS reads.
 //   A. (every wave) rank each list head among the wave's 64 heads; the K best go to LDS;
-//   B. (wave `lead`, lane = one of the W*K <= 64 survivors) rank the survivors; the K best heads' lists are kept;
-//   C. (wave `lead`, lane = one or two of the kept lists' K*KC entries) rank the entries; rank < K is the
+//   B. (wave 0, lane = one of the W*K <= 64 survivors) rank the survivors; the K best heads' lists are kept;
+//   C. (wave 0, lane = one or two of the kept lists' K*KC entries) rank the entries; rank < K is the
 //      output position.  Then the exact-prefix cut and the Rec rows as in merge_pod_body.
-// B and C are one wave's VALU chain: the merger workgroup's slots pass different `lead` waves, so their chains
-// issue on different SIMDs (the slots' waves 0 share SIMD 0: three chains on one SIMD's VALU).
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
@@ -302,7 +300,7 @@ __device__ __forceinline__ void wave_lds_order() {
 
 template <int KC, int K, bool COH, int MT, typename Sync>
 __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, const int tid, MergeSmem<KC, K, MT> &sm,
-                                               Sync sync, const int lead) {
+                                               Sync sync) {
     __builtin_amdgcn_s_setprio(3);  // latency-critical: win issue arbitration over co-resident score waves
     constexpr int W = MT / 64;
     static_assert(W * K <= 64, "survivors must fit one wave");
@@ -384,7 +382,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     }
     if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
     sync();
-    if (wave != lead) return;
+    if (wave != 0) return;
     if (dbg) ts[3] = __builtin_amdgcn_s_memtime();
     // B. rank the survivors (lane = slot); the K best heads' lists hold the pod's top K
     int ntot = 0;

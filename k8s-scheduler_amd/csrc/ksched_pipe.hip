@@ -1151,14 +1151,14 @@ __device__ __forceinline__ void serve_rescue(const PersistArgs &P, int id, int m
 
 // Pod m of batch b (p0 + m) against the nodes batch b - 2 committed (its export, ring slot (b - 2) % 4): the
 // keys at their current state, the predicate deltas since b's snapshot and the best entry -- what commit(b)
-// would otherwise compute for those inherited slots on its own critical path (commit_spc_batch, LAG3).  Wave `lead`
+// would otherwise compute for those inherited slots on its own critical path (commit_spc_batch, LAG3).  Wave 0
 // of the merger slot, lane = export entry; commit(b - 2) is done (the caller waited).  The key column goes to
 // inh keys[b % 4][m][0, n2), the summary to inh summary[b % 4][m]: {sum of deltas, best key, best idx | entry
 // << 32} (entry -1: none eligible).  Restated by oracle/cpu_ref.c commit_inherit (the two exports' deltas add).
 template <int PRIO, int DOM, bool LAB, bool F53>
-__device__ __forceinline__ void inherit_x2_keys(const PersistArgs &P, int64_t b, int m, int64_t pod, int mtid, int lead) {
-    if (mtid / 64 != lead) return;
-    const int lane = mtid % 64;
+__device__ __forceinline__ void inherit_x2_keys(const PersistArgs &P, int64_t b, int m, int64_t pod, int mtid) {
+    if (mtid >= 64) return;
+    const int lane = mtid;
     const XBuf *xb = reinterpret_cast<const XBuf *>(P.xring + (size_t)((b - 2) % 4) * P.xbuf_bytes);
     const uint64_t hdr = ld_coh(&xb->count);
     const int n2 = (uint32_t)(hdr >> 32) == (uint32_t)(b - 2) ? (int)(uint32_t)hdr : 0;
@@ -1212,7 +1212,6 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
     uint32_t *s_msg = reinterpret_cast<uint32_t *>(sbase + ML::ctl_bytes + ML::merge_bytes);  // this rank's list
     uint32_t *s_all = s_msg + msg_words(K);                                                     // every rank's list
     const int mtid = threadIdx.x % kMT;
-    const int lead = (g % kMS) % kMW;  // the wave of this slot that runs the merge's one-wave phases (merge_pod_fast)
     const int G = P.G;
     const int slot_prog = G + g;
     const int64_t NP = P.pods.p;
@@ -1278,7 +1277,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
             if (!mwait(b, &ctl->committed_x[g % kCtlReplicas].v, (unsigned long long)(b - 1), 6, kProgWaitCommit)) return;
             jitter_at(P.jitter, b, 3);
             for (int m = g; m < P.B; m += kMS * P.M)
-                if (p0 + m < NP) inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid, lead);
+                if (p0 + m < NP) inherit_x2_keys<PRIO, DOM, LAB, F53>(P, b, m, p0 + m, mtid);
         }
         if (!mwait(b, &ctl->arrive[slot].v, (use + 1) * (unsigned long long)G, 7, kProgWaitArrive)) return;
         if (mtid == 0 && g == 0) trace_at(P, b, 7);
@@ -1301,7 +1300,7 @@ __device__ __forceinline__ void merge_role(const PersistArgs &P, char *sbase, co
             // the pod's list is staged in LDS (the message the exchange sends, or the commit's list), so that it
             // leaves as 16-byte sc1 stores (an 8-byte sc1 store costs a whole memory write request)
             ma.lds_msg = p0 + m < NP ? s_msg : nullptr;
-            merge_pod_fast<KC, K, true, kMT>(ma, m, mtid, ms, sync, lead);
+            merge_pod_fast<KC, K, true, kMT>(ma, m, mtid, ms, sync);
             if (!xchg && p0 + m < NP) {
                 static_assert(K * sizeof(Rec) % 16 == 0, "a list is whole 16-byte chunks");
                 constexpr int kChunks = K * (int)sizeof(Rec) / 16;
