@@ -250,12 +250,14 @@ __device__ __forceinline__ void merge_pod_body(const MergeArgs &A, const int b, 
 
 // ------------------------------------------------------------------------------------------------
 // The same merge for the persistent pipeline's merge waves (MT = 256: W = 4 waves, one list per thread),
-// with ONE barrier and no LDS-latency-bound loops: every rank is counted over register broadcasts
-// (v_readlane of all 64 lanes) instead of LDS reads.
-//   A. (every wave) rank each list head among the wave's 64 heads; the K best go to LDS;
-//   B. (wave 0, lane = one of the W*K <= 64 survivors) rank the survivors; the K best heads' lists are kept;
-//   C. (wave 0, lane = one or two of the kept lists' K*KC entries) rank the entries; rank < K is the
-//      output position.  Then the exact-prefix cut and the Rec rows as in merge_pod_body.
+// with ONE barrier and no LDS-latency-bound loops: every selection is a register-only wave sort (DPP and
+// permlane swaps):
+//   A. (every wave) sort the wave's 64 list heads (wave_sort_desc); the K best go to LDS;
+//   B. (wave 0, lane = one of the W*K <= 64 survivors) sort the survivors; the K best heads' lists are kept;
+//   C. (wave 0, lane = one of the kept lists' K*KC <= 64 entries) sort the entries; lane r < K is output
+//      position r (K*KC > 64: rank each entry by rotations, wave_rank).
+// Then the exact-prefix cut and the Rec rows as in merge_pod_body.  (Round 6: the sorts replaced 63-rotation
+// rank counts -- cycles per merge 20.3k -> 15.2k, c4 merge leg p50 15.2 -> 12.1 us.)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
@@ -277,6 +279,50 @@ __device__ __forceinline__ int wave_rank(uint64_t code, int32_t idx, uint64_t mc
         r += code_better(((uint64_t)hi << 32) | lo, (int32_t)ix, mc, mi) ? 1 : 0;
     }
     return r;
+}
+
+// ---- a wave-wide sort of 64 (code, idx) pairs, best first (key desc, idx asc): the bitonic network in its
+// "flip" form, every comparator in one direction -- stage (M, HB) compares lane l with lane l ^ M, the lane
+// with bit HB clear keeps the better.  M = 2^k - 1 is the flip of the aligned 2^k block (its mirror), M = 2^j
+// the half-cleaners.  Every partner is a DPP or permlane swap (no LDS): xor 1/2/3 quad_perm, 7 row_half_mirror,
+// 15 row_mirror, 8 row_ror:8, 4 = 7 then 3, 16/32 the permlane swaps, 31 and 63 their compositions.  21 stages
+// of 3 partner words, a compare and 3 selects: ~2x fewer VALU instructions than 63 wave_ror1 rank rotations.
+template <int M>
+__device__ __forceinline__ uint32_t xpartner(uint32_t v) {
+    if constexpr (M == 1 || M == 2) return wpartner<M - 1>(v);
+    else if constexpr (M == 3) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x1B, 0xF, 0xF, false);
+    else if constexpr (M == 7) return wpartner<2>(v);
+    else if constexpr (M == 15) return wpartner<3>(v);
+    else if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false);
+    else if constexpr (M == 4) return xpartner<3>(xpartner<7>(v));
+    else if constexpr (M == 16) return wpartner<4>(v);
+    else if constexpr (M == 32) return wpartner<5>(v);
+    else if constexpr (M == 31) return xpartner<16>(xpartner<15>(v));
+    else { static_assert(M == 63, "partner"); return xpartner<32>(xpartner<16>(xpartner<15>(v))); }
+}
+template <int M, int HB>
+__device__ __forceinline__ void sort_stage(uint32_t &lo, uint32_t &hi, uint32_t &ix, const int lane) {
+    const uint32_t plo = xpartner<M>(lo), phi = xpartner<M>(hi), pix = xpartner<M>(ix);
+    const bool pb = code_better(((uint64_t)phi << 32) | plo, (int32_t)pix, ((uint64_t)hi << 32) | lo, (int32_t)ix);
+    const bool take = (lane & HB) ? !pb : pb;
+    lo = take ? plo : lo;
+    hi = take ? phi : hi;
+    ix = take ? pix : ix;
+}
+// On return lane r holds the wave's rank-r pair.  (code, idx) pairs are distinct except empty ones (0, kNoIdx).
+__device__ __forceinline__ void wave_sort_desc(uint64_t &code, int32_t &idx, const int lane) {
+    uint32_t lo = (uint32_t)code, hi = (uint32_t)(code >> 32), ix = (uint32_t)idx;
+    sort_stage<1, 1>(lo, hi, ix, lane);
+    sort_stage<3, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
+    sort_stage<7, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
+    sort_stage<15, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane);
+    sort_stage<1, 1>(lo, hi, ix, lane);
+    sort_stage<31, 16>(lo, hi, ix, lane); sort_stage<8, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane);
+    sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
+    sort_stage<63, 32>(lo, hi, ix, lane); sort_stage<16, 16>(lo, hi, ix, lane); sort_stage<8, 8>(lo, hi, ix, lane);
+    sort_stage<4, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
+    code = ((uint64_t)hi << 32) | lo;
+    idx = (int32_t)ix;
 }
 
 // The touched-node screen's threshold of a merged list (lane = output entry; okm: the valid entries, a prefix;
@@ -370,15 +416,14 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         const int nv = __popcll(__ballot(idx[0] != kNoIdx));
         if (lane == 0) { sm.wck[wave] = bc; sm.wci[wave] = bi; sm.wcut[wave] = wcut; sm.wcnt[wave] = wc; sm.wnv[wave] = nv; }
     }
-    // A. rank each head within its wave
+    // A. the wave's heads sorted: lanes < K hold its K best (an empty list's head (0, kNoIdx) sorts last and is
+    // written as the empty slot it replaces)
     {
-        const int rk = wave_rank(code[0], idx[0], code[0], idx[0]);
+        uint64_t hc = code[0];
+        int32_t hx = idx[0];
+        wave_sort_desc(hc, hx, lane);
         wave_lds_order();  // the slot initialisation above precedes every survivor write of this wave
-        if (idx[0] != kNoIdx && rk < K) {
-            sm.ccode[wave * K + rk] = code[0];
-            sm.cidx[wave * K + rk] = idx[0];
-            sm.clist[wave * K + rk] = tid;
-        }
+        if (lane < K) { sm.ccode[wave * K + lane] = hc; sm.cidx[wave * K + lane] = hx; }
     }
     if (dbg) ts[2] = __builtin_amdgcn_s_memtime();
     sync();
@@ -390,11 +435,11 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     for (int w = 0; w < W; ++w) ntot += sm.wnv[w];
     {
         const bool in = lane < W * K;
-        const uint64_t sc = in ? sm.ccode[lane] : 0ull;
-        const int32_t si = in ? sm.cidx[lane] : kNoIdx;
-        const int32_t sl = in ? sm.clist[lane] : 0;
-        const int g = wave_rank(sc, si, sc, si);
-        if (si != kNoIdx && g < K) sm.keep[g] = sl;
+        uint64_t sc = in ? sm.ccode[lane] : 0ull;
+        int32_t si = in ? sm.cidx[lane] : kNoIdx;
+        wave_sort_desc(sc, si, lane);
+        // a head's list is its score workgroup's: workgroup g holds the nodes idx - node_offset = g (mod C_in)
+        if (lane < K && si != kNoIdx) sm.keep[lane] = (int32_t)((si - (int32_t)A.node_offset) % A.C_in);
     }
     wave_lds_order();
     if (dbg) ts[4] = __builtin_amdgcn_s_memtime();
@@ -412,12 +457,17 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         ei[p] = in ? sm.idx[l][e % KC] : kNoIdx;
         nvalid += __popcll(__ballot(ei[p] != kNoIdx));
     }
+    if constexpr (EP == 1) {
+        wave_sort_desc(ec[0], ei[0], lane);  // lane r: the rank-r entry
+        if (lane < K && ei[0] != kNoIdx) { sm.ocode[lane] = ec[0]; sm.oidx[lane] = ei[0]; }
+    } else {
 #pragma unroll
-    for (int p = 0; p < EP; ++p) {
-        int r = 0;
+        for (int p = 0; p < EP; ++p) {
+            int r = 0;
 #pragma unroll
-        for (int p2 = 0; p2 < EP; ++p2) r += wave_rank(ec[p2], ei[p2], ec[p], ei[p]);
-        if (ei[p] != kNoIdx && r < K) { sm.ocode[r] = ec[p]; sm.oidx[r] = ei[p]; }
+            for (int p2 = 0; p2 < EP; ++p2) r += wave_rank(ec[p2], ei[p2], ec[p], ei[p]);
+            if (ei[p] != kNoIdx && r < K) { sm.ocode[r] = ec[p]; sm.oidx[r] = ei[p]; }
+        }
     }
     wave_lds_order();
     if (dbg) ts[5] = __builtin_amdgcn_s_memtime();
