@@ -309,18 +309,30 @@ __device__ __forceinline__ void sort_stage(uint32_t &lo, uint32_t &hi, uint32_t 
     hi = take ? phi : hi;
     ix = take ? pix : ix;
 }
-// On return lane r holds the wave's rank-r pair.  (code, idx) pairs are distinct except empty ones (0, kNoIdx).
+// Lanes hold sorted runs of RUN pairs (aligned; RUN = 1: anything): the stages of the block sizes above RUN merge
+// them.  On return lane r holds the wave's rank-r pair.  (code, idx) pairs are distinct except empty ones (0, kNoIdx).
+template <int RUN>
 __device__ __forceinline__ void wave_sort_desc(uint64_t &code, int32_t &idx, const int lane) {
+    static_assert(RUN == 1 || RUN == 2 || RUN == 4 || RUN == 8 || RUN == 16 || RUN == 32, "runs");
     uint32_t lo = (uint32_t)code, hi = (uint32_t)(code >> 32), ix = (uint32_t)idx;
-    sort_stage<1, 1>(lo, hi, ix, lane);
-    sort_stage<3, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
-    sort_stage<7, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
-    sort_stage<15, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane);
-    sort_stage<1, 1>(lo, hi, ix, lane);
-    sort_stage<31, 16>(lo, hi, ix, lane); sort_stage<8, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane);
+    if constexpr (RUN <= 1) sort_stage<1, 1>(lo, hi, ix, lane);
+    if constexpr (RUN <= 2) { sort_stage<3, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane); }
+    if constexpr (RUN <= 4) {
+        sort_stage<7, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane);
+        sort_stage<1, 1>(lo, hi, ix, lane);
+    }
+    if constexpr (RUN <= 8) {
+        sort_stage<15, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane);
+        sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
+    }
+    if constexpr (RUN <= 16) {
+        sort_stage<31, 16>(lo, hi, ix, lane); sort_stage<8, 8>(lo, hi, ix, lane);
+        sort_stage<4, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane);
+        sort_stage<1, 1>(lo, hi, ix, lane);
+    }
+    sort_stage<63, 32>(lo, hi, ix, lane); sort_stage<16, 16>(lo, hi, ix, lane);
+    sort_stage<8, 8>(lo, hi, ix, lane); sort_stage<4, 4>(lo, hi, ix, lane);
     sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
-    sort_stage<63, 32>(lo, hi, ix, lane); sort_stage<16, 16>(lo, hi, ix, lane); sort_stage<8, 8>(lo, hi, ix, lane);
-    sort_stage<4, 4>(lo, hi, ix, lane); sort_stage<2, 2>(lo, hi, ix, lane); sort_stage<1, 1>(lo, hi, ix, lane);
     code = ((uint64_t)hi << 32) | lo;
     idx = (int32_t)ix;
 }
@@ -421,7 +433,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     {
         uint64_t hc = code[0];
         int32_t hx = idx[0];
-        wave_sort_desc(hc, hx, lane);
+        wave_sort_desc<1>(hc, hx, lane);
         wave_lds_order();  // the slot initialisation above precedes every survivor write of this wave
         if (lane < K) { sm.ccode[wave * K + lane] = hc; sm.cidx[wave * K + lane] = hx; }
     }
@@ -437,7 +449,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         const bool in = lane < W * K;
         uint64_t sc = in ? sm.ccode[lane] : 0ull;
         int32_t si = in ? sm.cidx[lane] : kNoIdx;
-        wave_sort_desc(sc, si, lane);
+        wave_sort_desc<K>(sc, si, lane);  // the W waves' K survivors are sorted runs: only the merge stages
         // a head's list is its score workgroup's: workgroup g holds the nodes idx - node_offset = g (mod C_in)
         if (lane < K && si != kNoIdx) sm.keep[lane] = (int32_t)((si - (int32_t)A.node_offset) % A.C_in);
     }
@@ -458,7 +470,7 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
         nvalid += __popcll(__ballot(ei[p] != kNoIdx));
     }
     if constexpr (EP == 1) {
-        wave_sort_desc(ec[0], ei[0], lane);  // lane r: the rank-r entry
+        wave_sort_desc<1>(ec[0], ei[0], lane);  // lane r: the rank-r entry
         if (lane < K && ei[0] != kNoIdx) { sm.ocode[lane] = ec[0]; sm.oidx[lane] = ei[0]; }
     } else {
 #pragma unroll
@@ -494,9 +506,9 @@ __device__ __forceinline__ void merge_pod_fast(const MergeArgs &A, const int b, 
     if (lane < K) {
         Rec r{};
         if (ok) {
-            const NodeRec &nd = A.nodes[mi - A.node_offset];
             const uint64_t u = (mc >> 63) ? (mc & 0x7fffffffffffffffull) : ~mc;  // inverse of key_code
             r.key = __longlong_as_double((long long)u); r.idx = mi; r.valid = 1;
+            const NodeRec &nd = A.nodes[mi - A.node_offset];
             r.a[0] = load_i64<COH>(&nd.a[0]); r.a[1] = load_i64<COH>(&nd.a[1]); r.a[2] = load_i64<COH>(&nd.a[2]);
             r.labels = nd.labels; r.price = nd.price;  // never written during a call
         } else {
