@@ -28,7 +28,7 @@ FLOPS_PER_PAIR = 28          # 10 div + 18 add/sub/mul per resource-s
 # PMC summaries of the same workloads (tools/pmc_summary.py over separate FETCH_SIZE / WRITE_SIZE / SQ
 # passes of `bench.py` itself); keyed by (kernel, config, batch, ranks)
 PMC_SUMMARIES = {
-    ("k_pipe", "c4", 64, 1): os.path.join(ROOT, "profiles", "r06_pmc_c4_pipe.json"),
+    ("k_pipe", "c4", 64, 1): os.path.join(ROOT, "profiles", "r06b_pmc_c4_pipe.json"),
     ("k_score_topk", "c4", 64, 1): os.path.join(ROOT, "profiles", "r01_pmc_c4_b64.json"),
 }
 
